@@ -1,0 +1,140 @@
+/*
+ * mm.h — C-ABI of the MI355X-native MotionMagnificationProcessor frame operator.
+ *
+ * Drop-in boundary for the reference Unity component
+ *   [RequireComponent(typeof(Camera))] public class MotionMagnificationProcessor
+ *   (Assets/Scripts/MotionMagnificationProcessor.cs:4-5)
+ * whose per-frame entry point is the image-effect callback
+ *   void OnRenderImage(RenderTexture source, RenderTexture destination)  (.cs:101)
+ * An RGBA frame goes in, the PhaseScale-amplified frame comes out.
+ *
+ * Conventions
+ *   - Every function returns MM_OK (0) or a negative MM_ERR_* code; nothing
+ *     throws or aborts across the ABI.  mm_strerror() names a code.
+ *   - Frames are caller-owned, row-major, H rows of W RGBA pixels, tightly
+ *     packed (pitch = W * bytes-per-pixel).  RGBA8 is UNORM (v = byte/255);
+ *     RGBA32F is linear float.  The handle owns all device scratch and the
+ *     one-frame temporal state.
+ *   - A handle is not thread-safe: one handle per video stream, calls in frame
+ *     order (Unity calls OnRenderImage serially on its render thread).
+ *   - The first frame after mm_create/mm_reset is passed through bitwise
+ *     (alpha included) and becomes the temporal state (.cs:111-117); after
+ *     that output alpha is 1 (CombineYIQChannels.shader:56).
+ *   - W and H must be even, max(W,H) <= 4096 (padded square N = nextpow2).
+ */
+#ifndef MM_H
+#define MM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MM_ABI_VERSION 1
+
+/* error codes */
+#define MM_OK               0
+#define MM_ERR_INVALID     -1  /* bad argument / handle */
+#define MM_ERR_UNSUPPORTED -2  /* geometry or mode not supported by this build */
+#define MM_ERR_HIP         -3  /* HIP runtime error (launch, copy, ...) */
+#define MM_ERR_NO_DEVICE   -4  /* no usable gfx950 device */
+#define MM_ERR_OOM         -5  /* device allocation failed */
+#define MM_ERR_NO_STATE    -6  /* mm_get_state before any frame was seen */
+
+/* frame formats */
+#define MM_RGBA8   0
+#define MM_RGBA32F 1
+
+/* mm_params.mode */
+#define MM_MODE_PYRAMID   0   /* usePyramidDecomposition = true (.cs:18, :128-131) */
+/* mm_params.edge_mode: sampler wrap of the engine resamples and the blur
+ * (unpinned by the reference) */
+#define MM_EDGE_REPEAT 0
+#define MM_EDGE_CLAMP  1
+
+/* mm_process flags */
+#define MM_FRAMES_ON_DEVICE 1  /* in/out are device pointers (else host memory) */
+
+typedef struct mm_handle mm_handle;
+
+/* Inspector fields of the reference component (.cs:12-31). */
+typedef struct {
+    int   levels;              /* pyramidLevels            .cs:19  (1..16)      */
+    float min_freq;            /* minFrequency             .cs:20               */
+    float max_freq;            /* maxFrequency             .cs:21               */
+    float phase_scale;         /* phaseScale (PhaseScale)  .cs:29               */
+    float magnitude_threshold; /* magnitudeThreshold=0.01  .cs:30               */
+    int   orientations;        /* extension; must be 1 (reference semantics)    */
+    int   mode;                /* MM_MODE_PYRAMID                               */
+    int   edge_mode;           /* MM_EDGE_REPEAT | MM_EDGE_CLAMP                */
+    int   apply_magnification; /* applyMotionMagnification .cs:12 (0: passthrough) */
+} mm_params;
+
+/* Reference defaults: levels 5, 0.05/0.45, phaseScale 10, threshold 0.01. */
+int mm_params_default(mm_params *p);
+
+/* Start()/InitializeProcessor (.cs:90-94, :289-342): geometry frozen here. */
+int mm_create(int width, int height, const mm_params *p, int hip_device,
+              mm_handle **out);
+
+/* OnValidate (.cs:78-88): new parameters apply from the next frame. */
+int mm_set_params(mm_handle *h, const mm_params *p);
+int mm_get_params(const mm_handle *h, mm_params *p);
+
+/* Padded FFT size N (.cs:300-302). */
+int mm_padded_size(const mm_handle *h, int *n);
+
+/* OnRenderImage (.cs:101-143): one frame in, one frame out.
+ * flags & MM_FRAMES_ON_DEVICE: in/out are device pointers and the call is
+ * asynchronous on `hip_stream` (NULL = the handle's stream); otherwise in/out
+ * are host pointers and the call returns when out is written. */
+int mm_process(mm_handle *h, const void *in, void *out, int format, int flags,
+               void *hip_stream);
+
+/* Consecutive frames of one stream in a single call (device pointers;
+ * frame k at in + k*W*H*bpp).  Equivalent, frame for frame, to `count`
+ * mm_process calls; batches the launches. Asynchronous on hip_stream. */
+int mm_process_stream(mm_handle *h, const void *in, void *out, int count,
+                      int format, void *hip_stream);
+
+/* isFirstFrame = true (.cs:75): the next frame is passed through. */
+int mm_reset(mm_handle *h);
+
+/* The temporal state carried between frames: the previous frame's spectrum
+ * (what previousSourceTexture, .cs:142, is used for).  `dev_buf` is device
+ * memory of mm_state_size() bytes.  Ordered on hip_stream (NULL = handle's). */
+int mm_state_size(const mm_handle *h, size_t *bytes);
+int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream);
+int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stream);
+/* Compute the state that frame `in` would leave behind (its spectrum) into
+ * dev_buf without touching the handle's own state (used by the multi-GPU ring
+ * to hand the chunk-boundary state to the next rank). */
+int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf,
+                     size_t bytes, void *hip_stream);
+
+/* The handle's HIP stream (hipStream_t). */
+void *mm_stream(mm_handle *h);
+
+/* OnDestroy/ReleaseResources (.cs:96-99, :344-356). */
+void mm_destroy(mm_handle *h);
+
+const char *mm_strerror(int code);
+int mm_abi_version(void);
+
+/* ---- utilities (not on the reference surface) ---- */
+/* Synthetic stream frames generated on the device:
+ * frames t0..t0+count-1 into dev_out (RGBA8). */
+int mm_synth_frames(void *dev_out, int width, int height, int t0, int count,
+                    uint64_t seed, int gray, void *hip_stream);
+
+/* Host-side geometry tables (no GPU needed), exposed for tests:
+ * per image column (row) the 4 source indices and 4 weights of the composite
+ * stretch+pad bilinear resample, including the Hann window factor. */
+int mm_resample_table(int width, int height, int axis, int edge_mode,
+                      int32_t *idx4, float *w4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,608 @@
+// mm_api.hip — C-ABI implementation (include/mm.h) of the MI355X-native
+// MotionMagnificationProcessor frame operator.
+//
+// Reference surface (Assets/Scripts/MotionMagnificationProcessor.cs):
+//   Start/InitializeProcessor :90-94,:289-342 -> mm_create
+//   OnValidate                :78-88          -> mm_set_params
+//   OnRenderImage             :101-143        -> mm_process / mm_process_stream
+//   OnDestroy/ReleaseResources:96-99,:344-356 -> mm_destroy
+// There is no CPU fallback: every frame is computed by the HIP kernels of
+// mm_kernels.hpp; without a gfx950 device mm_create fails with MM_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/mm.h"
+#include "mm_kernels.hpp"
+
+using namespace mm;
+
+#define HIPCHK(x)                                                             \
+    do {                                                                      \
+        hipError_t e_ = (x);                                                  \
+        if (e_ != hipSuccess) {                                               \
+            if (getenv("MM_DEBUG"))                                           \
+                fprintf(stderr, "mm355: %s failed: %s (%s:%d)\n", #x,         \
+                        hipGetErrorString(e_), __FILE__, __LINE__);           \
+            return MM_ERR_HIP;                                                \
+        }                                                                     \
+    } while (0)
+
+struct mm_handle {
+    int W, H, N, log2n, device;
+    mm_params p;
+    hipStream_t stream;
+    Geo geo;
+    Spec spec;
+    Blur5 blur;
+    Tap4 *d_col, *d_row;
+    c2 *d_tw;
+    c2 *d_G, *d_Q, *d_state;
+    size_t g_stride, q_stride;  // elements per frame
+    int chunk;                  // frames per K1/K2/K3 batch
+    uint8_t *d_stage_in, *d_stage_out;
+    size_t stage_bytes;
+    bool has_state;
+};
+
+// ------------------------------------------------------------------------
+// host tables
+// ------------------------------------------------------------------------
+static int wrap_host(int i, int n, int edge)
+{
+    if (edge) return i < 0 ? 0 : (i >= n ? n - 1 : i);
+    int r = i % n;
+    return r < 0 ? r + n : r;
+}
+
+static int next_pow2(int v)
+{
+    int n = 1;
+    while (n < v) n <<= 1;
+    return n;
+}
+
+// Composite of the stretch blit (src S texels -> N, RGBToYIQ pass, .cs:147) and
+// the PadTexture quad resample (N -> S texels placed at (N-S)/2, .cs:358-381),
+// both bilinear at texel t = u*size - 0.5, times the Hann window of the canvas
+// position (WindowingFunction.shader:47-70).  fp32 formulas as the oracle.
+static void build_tab(int S, int N, int edge, std::vector<Tap4> &tab)
+{
+    tab.resize(S);
+    const int off = (N - S) / 2;
+    for (int i = 0; i < S; ++i) {
+        const int X = off + i;
+        const float u = (float)(2 * X + 1 - (N - S)) / (float)(2 * S);
+        const float tp = u * (float)N - 0.5f;
+        const float af = floorf(tp);
+        const int a = (int)af;
+        const float gfr = tp - af;
+        Tap4 e;
+        for (int k = 0; k < 2; ++k) {
+            const int aa = wrap_host(a + k, N, edge);
+            const float us = ((float)aa + 0.5f) / (float)N;
+            const float ts = us * (float)S - 0.5f;
+            const float bf = floorf(ts);
+            const int b = (int)bf;
+            const float fr = ts - bf;
+            const float wk = k ? gfr : 1.0f - gfr;
+            e.idx[2 * k] = wrap_host(b, S, edge);
+            e.w[2 * k] = wk * (1.0f - fr);
+            e.idx[2 * k + 1] = wrap_host(b + 1, S, edge);
+            e.w[2 * k + 1] = wk * fr;
+        }
+        const float wu = ((float)X + 0.5f) / (float)N;
+        const float hann = 0.5f * (1.0f - cosf(2.0f * kPi * wu));
+        for (int m = 0; m < 4; ++m) e.w[m] *= hann;
+        tab[i] = e;
+    }
+}
+
+static void build_spec(const mm_params &p, int N, Spec &sp)
+{
+    memset(&sp, 0, sizeof(sp));
+    sp.L = p.levels;
+    sp.minF = p.min_freq;
+    sp.maxF = p.max_freq;
+    sp.S = p.phase_scale;
+    sp.tau = p.magnitude_threshold;
+    sp.inv_nn = 1.0f / ((float)N * (float)N);
+    for (int i = 1; i < p.levels - 1; ++i) {
+        // PyramidOperations.compute:59-64 (L=3: 0/0 = NaN -> empty band)
+        volatile float num = (float)(i - 1), den = (float)(p.levels - 3);
+        const float ratio = num / den;
+        const float center = p.min_freq * powf(p.max_freq / p.min_freq, 1.0f - ratio);
+        const float bwid = center * 0.5f;
+        sp.lo[i] = center - bwid;
+        sp.hi[i] = center + bwid;
+    }
+}
+
+// GaussianBlur.shader:47-60 at _BlurSize 0.5 (.cs:427): bilinear taps at
+// +-0.6923 and +-1.6154 texels == a 5-tap FIR.
+static Blur5 build_blur()
+{
+    const double c0 = 0.2270270270, c1 = 0.3162162162, c2w = 0.0702702703;
+    const double f1 = 0.5 * 1.3846153846, f2 = 0.5 * 3.2307692308 - 1.0;
+    Blur5 b;
+    b.w0 = (float)(c0 + 2.0 * c1 * (1.0 - f1));
+    b.w1 = (float)(c1 * f1 + c2w * (1.0 - f2));
+    b.w2 = (float)(c2w * f2);
+    return b;
+}
+
+static int validate_params(const mm_params *p)
+{
+    if (!p) return MM_ERR_INVALID;
+    if (p->levels < 1 || p->levels > kMaxLevels) return MM_ERR_UNSUPPORTED;
+    if (p->orientations != 1) return MM_ERR_UNSUPPORTED;
+    if (p->mode != MM_MODE_PYRAMID) return MM_ERR_UNSUPPORTED;
+    if (p->edge_mode != MM_EDGE_REPEAT && p->edge_mode != MM_EDGE_CLAMP) return MM_ERR_INVALID;
+    if (!(p->min_freq > 0.0f) || !(p->max_freq > 0.0f)) return MM_ERR_INVALID;
+    return MM_OK;
+}
+
+// ------------------------------------------------------------------------
+// launches
+// ------------------------------------------------------------------------
+template <int LOG2N> static size_t lds_fft_bytes()
+{
+    return sizeof(c2) * (size_t)groups_per_wg<LOG2N>() * lds_complex<(1 << LOG2N)>();
+}
+template <int LOG2N> static size_t lds_k3_bytes(int W)
+{
+    return lds_fft_bytes<LOG2N>() + sizeof(float) * (size_t)k3_ring<LOG2N>() * W;
+}
+
+template <int LOG2N>
+static int set_attrs(int W)
+{
+    const size_t k3 = lds_k3_bytes<LOG2N>(W);
+    HIPCHK(hipFuncSetAttribute((const void *)k_rows_inv<LOG2N, 0>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3));
+    HIPCHK(hipFuncSetAttribute((const void *)k_rows_inv<LOG2N, 1>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3));
+    return MM_OK;
+}
+
+static int k3_band_rows(const mm_handle *h, int nframes)
+{
+    // enough work-groups to fill 256 CUs, bands >= 8 rows to bound the 4-row halo
+    const int target = 1024;
+    int br = (int)(((long long)h->H * nframes + target - 1) / target);
+    br = std::max(br, 8);
+    br = (br + 1) & ~1;
+    return std::min(br, h->H);
+}
+
+template <int LOG2N>
+static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipStream_t s)
+{
+    const int ppf = h->H / 2;
+    const int total = ppf * nframes;
+    const int gpw = groups_per_wg<LOG2N>();
+    const int blocks = (total + gpw - 1) / gpw;
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    if (fmt == MM_RGBA8)
+        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(wg_threads<LOG2N>()),
+                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col,
+                           h->d_row, h->d_tw, h->d_G, h->g_stride);
+    else
+        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(wg_threads<LOG2N>()),
+                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col,
+                           h->d_row, h->d_tw, h->d_G, h->g_stride);
+    HIPCHK(hipGetLastError());
+    return MM_OK;
+}
+
+template <int LOG2N>
+static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 *st_in,
+                     c2 *st_out, hipStream_t s)
+{
+    const int gpw = groups_per_wg<LOG2N>();
+    const int cols = (1 << LOG2N) / 2 + 1;
+    const int blocks = (cols + gpw - 1) / gpw;
+    hipLaunchKernelGGL((k_cols<LOG2N>), dim3(blocks), dim3(wg_threads<LOG2N>()),
+                       lds_fft_bytes<LOG2N>(), s, h->d_G, h->g_stride, h->d_Q, h->q_stride,
+                       st_in, st_out, nframes, first_passthrough, h->geo, h->spec, h->d_tw);
+    HIPCHK(hipGetLastError());
+    return MM_OK;
+}
+
+template <int LOG2N>
+static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, int nframes,
+                     int fmt, hipStream_t s)
+{
+    const int nout = nframes - frame0;
+    if (nout <= 0) return MM_OK;
+    const int br = k3_band_rows(h, nout);
+    const int bands = (h->H + br - 1) / br;
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t lds = lds_k3_bytes<LOG2N>(h->W);
+    if (fmt == MM_RGBA8)
+        hipLaunchKernelGGL((k_rows_inv<LOG2N, 0>), dim3(bands * nout), dim3(wg_threads<LOG2N>()),
+                           lds, s, h->d_Q, h->q_stride, in, out, fb, frame0, bands, br, h->geo,
+                           h->blur, h->d_col, h->d_row, h->d_tw);
+    else
+        hipLaunchKernelGGL((k_rows_inv<LOG2N, 1>), dim3(bands * nout), dim3(wg_threads<LOG2N>()),
+                           lds, s, h->d_Q, h->q_stride, in, out, fb, frame0, bands, br, h->geo,
+                           h->blur, h->d_col, h->d_row, h->d_tw);
+    HIPCHK(hipGetLastError());
+    return MM_OK;
+}
+
+// One batch of `n` consecutive frames (n <= chunk), all on the device.
+template <int LOG2N>
+static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int fmt,
+                     hipStream_t s)
+{
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const int first = h->has_state ? 0 : 1;
+    int rc;
+    if (first) HIPCHK(hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s));
+    if (!h->p.apply_magnification) {
+        // applyMotionMagnification == false: Blit(source, destination) (.cs:139),
+        // but previousSourceTexture still follows the input (.cs:142).
+        const int from = first ? 1 : 0;
+        if (n > from)
+            HIPCHK(hipMemcpyAsync(out + fb * from, in + fb * from, fb * (n - from),
+                                  hipMemcpyDeviceToDevice, s));
+        if ((rc = launch_k1<LOG2N>(h, in + fb * (n - 1), 1, fmt, s))) return rc;
+        if ((rc = launch_k2<LOG2N>(h, 1, 1, nullptr, h->d_state, s))) return rc;
+        h->has_state = true;
+        return MM_OK;
+    }
+    if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s))) return rc;
+    if ((rc = launch_k2<LOG2N>(h, n, first, first ? nullptr : h->d_state, h->d_state, s)))
+        return rc;
+    if ((rc = launch_k3<LOG2N>(h, in, out, first, n, fmt, s))) return rc;
+    h->has_state = true;
+    return MM_OK;
+}
+
+template <int LOG2N>
+static int run_stream(mm_handle *h, const uint8_t *in, uint8_t *out, int count, int fmt,
+                      hipStream_t s)
+{
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    for (int f0 = 0; f0 < count; f0 += h->chunk) {
+        const int n = std::min(h->chunk, count - f0);
+        int rc = run_chunk<LOG2N>(h, in + fb * f0, out + fb * f0, n, fmt, s);
+        if (rc) return rc;
+    }
+    return MM_OK;
+}
+
+template <int LOG2N>
+static int compute_state(mm_handle *h, const uint8_t *in, int fmt, c2 *dst, hipStream_t s)
+{
+    int rc;
+    if ((rc = launch_k1<LOG2N>(h, in, 1, fmt, s))) return rc;
+    return launch_k2<LOG2N>(h, 1, 1, nullptr, dst, s);
+}
+
+#define MM_DISPATCH(expr_template)                          \
+    switch (h->log2n) {                                     \
+    case 4: return expr_template(4);                        \
+    case 5: return expr_template(5);                        \
+    case 6: return expr_template(6);                        \
+    case 7: return expr_template(7);                        \
+    case 8: return expr_template(8);                        \
+    case 9: return expr_template(9);                        \
+    case 10: return expr_template(10);                      \
+    case 11: return expr_template(11);                      \
+    case 12: return expr_template(12);                      \
+    default: return MM_ERR_UNSUPPORTED;                     \
+    }
+
+static int do_set_attrs(mm_handle *h)
+{
+#define X(L) set_attrs<L>(h->W)
+    MM_DISPATCH(X)
+#undef X
+}
+static int do_stream(mm_handle *h, const uint8_t *in, uint8_t *out, int count, int fmt,
+                     hipStream_t s)
+{
+#define X(L) run_stream<L>(h, in, out, count, fmt, s)
+    MM_DISPATCH(X)
+#undef X
+}
+static int do_compute_state(mm_handle *h, const uint8_t *in, int fmt, c2 *dst, hipStream_t s)
+{
+#define X(L) compute_state<L>(h, in, fmt, dst, s)
+    MM_DISPATCH(X)
+#undef X
+}
+
+// ------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------
+extern "C" {
+
+int mm_abi_version(void) { return MM_ABI_VERSION; }
+
+const char *mm_strerror(int code)
+{
+    switch (code) {
+    case MM_OK: return "ok";
+    case MM_ERR_INVALID: return "invalid argument";
+    case MM_ERR_UNSUPPORTED: return "unsupported geometry or mode";
+    case MM_ERR_HIP: return "HIP runtime error";
+    case MM_ERR_NO_DEVICE: return "no gfx950 device";
+    case MM_ERR_OOM: return "device out of memory";
+    case MM_ERR_NO_STATE: return "no temporal state yet";
+    default: return "unknown error";
+    }
+}
+
+int mm_params_default(mm_params *p)
+{
+    if (!p) return MM_ERR_INVALID;
+    p->levels = 5;                 // .cs:19
+    p->min_freq = 0.05f;           // .cs:20
+    p->max_freq = 0.45f;           // .cs:21
+    p->phase_scale = 10.0f;        // .cs:29
+    p->magnitude_threshold = 0.01f;// .cs:30
+    p->orientations = 1;
+    p->mode = MM_MODE_PYRAMID;
+    p->edge_mode = MM_EDGE_REPEAT;
+    p->apply_magnification = 1;    // .cs:12
+    return MM_OK;
+}
+
+int mm_resample_table(int width, int height, int axis, int edge_mode, int32_t *idx4, float *w4)
+{
+    if (width <= 0 || height <= 0 || !idx4 || !w4 || (axis != 0 && axis != 1)) return MM_ERR_INVALID;
+    const int N = next_pow2(std::max(width, height));
+    const int S = axis == 0 ? width : height;
+    std::vector<Tap4> tab;
+    build_tab(S, N, edge_mode, tab);
+    for (int i = 0; i < S; ++i)
+        for (int m = 0; m < 4; ++m) {
+            idx4[i * 4 + m] = tab[i].idx[m];
+            w4[i * 4 + m] = tab[i].w[m];
+        }
+    return MM_OK;
+}
+
+static void free_handle(mm_handle *h)
+{
+    if (!h) return;
+    (void)hipFree(h->d_col);
+    (void)hipFree(h->d_row);
+    (void)hipFree(h->d_tw);
+    (void)hipFree(h->d_G);
+    (void)hipFree(h->d_Q);
+    (void)hipFree(h->d_state);
+    (void)hipFree(h->d_stage_in);
+    (void)hipFree(h->d_stage_out);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+static int upload_tables(mm_handle *h)
+{
+    std::vector<Tap4> col, row;
+    build_tab(h->W, h->N, h->p.edge_mode, col);
+    build_tab(h->H, h->N, h->p.edge_mode, row);
+    HIPCHK(hipMemcpy(h->d_col, col.data(), sizeof(Tap4) * h->W, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_row, row.data(), sizeof(Tap4) * h->H, hipMemcpyHostToDevice));
+    return MM_OK;
+}
+
+int mm_create(int width, int height, const mm_params *p, int hip_device, mm_handle **out)
+{
+    if (!out) return MM_ERR_INVALID;
+    *out = nullptr;
+    if (width < 2 || height < 2 || (width & 1) || (height & 1)) return MM_ERR_UNSUPPORTED;
+    int rc = validate_params(p);
+    if (rc) return rc;
+    const int N = next_pow2(std::max(std::max(width, height), 16));
+    if (N > 4096) return MM_ERR_UNSUPPORTED;
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MM_ERR_NO_DEVICE;
+    if (hip_device < 0 || hip_device >= ndev) return MM_ERR_INVALID;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) return MM_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MM_ERR_NO_DEVICE;
+    HIPCHK(hipSetDevice(hip_device));
+
+    mm_handle *h = new (std::nothrow) mm_handle();
+    if (!h) return MM_ERR_OOM;
+    h->W = width;
+    h->H = height;
+    h->N = N;
+    h->log2n = 0;
+    while ((1 << h->log2n) < N) ++h->log2n;
+    h->device = hip_device;
+    h->p = *p;
+    Geo &g = h->geo;
+    g.W = width;
+    g.H = height;
+    g.N = N;
+    g.x0 = (N - width) / 2;   // PadTexture offsets (.cs:360-363)
+    g.y0 = (N - height) / 2;
+    g.rb = g.y0 - 2;
+    g.Hn = std::min(height + 4, N);
+    g.Hq = (g.Hn + 1) & ~1;
+    g.edge = p->edge_mode;
+    build_spec(*p, N, h->spec);
+    h->blur = build_blur();
+
+    const char *ch = getenv("MM_CHUNK");
+    h->chunk = ch ? std::max(1, atoi(ch)) : (N >= 4096 ? 4 : 8);
+    h->g_stride = (size_t)(N / 2 + 1) * height;
+    h->q_stride = (size_t)(N / 2 + 1) * g.Hq;
+
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        free_handle(h);
+        return MM_ERR_HIP;
+    }
+    bool ok = hipMalloc(&h->d_col, sizeof(Tap4) * width) == hipSuccess &&
+              hipMalloc(&h->d_row, sizeof(Tap4) * height) == hipSuccess &&
+              hipMalloc(&h->d_tw, sizeof(c2) * N) == hipSuccess &&
+              hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * h->chunk) == hipSuccess &&
+              hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * h->chunk) == hipSuccess &&
+              hipMalloc(&h->d_state, sizeof(c2) * (size_t)(N / 2 + 1) * N) == hipSuccess;
+    if (!ok) {
+        free_handle(h);
+        return MM_ERR_OOM;
+    }
+    std::vector<c2> tw(N);
+    for (int k = 0; k < N; ++k) {
+        const double a = -2.0 * M_PI * (double)k / (double)N;
+        tw[k].x = (float)cos(a);
+        tw[k].y = (float)sin(a);
+    }
+    if (hipMemcpy(h->d_tw, tw.data(), sizeof(c2) * N, hipMemcpyHostToDevice) != hipSuccess ||
+        upload_tables(h) != MM_OK || do_set_attrs(h) != MM_OK) {
+        free_handle(h);
+        return MM_ERR_HIP;
+    }
+    h->has_state = false;
+    if (getenv("MM_DEBUG"))
+        fprintf(stderr, "mm355: Original: %dx%d, Padded: %dx%d\n", width, height, N, N);  // .cs:304
+    *out = h;
+    return MM_OK;
+}
+
+int mm_set_params(mm_handle *h, const mm_params *p)
+{
+    if (!h) return MM_ERR_INVALID;
+    int rc = validate_params(p);
+    if (rc) return rc;
+    const bool edge_changed = p->edge_mode != h->p.edge_mode;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->p = *p;
+    h->geo.edge = p->edge_mode;
+    build_spec(*p, h->N, h->spec);
+    if (edge_changed) return upload_tables(h);
+    return MM_OK;
+}
+
+int mm_get_params(const mm_handle *h, mm_params *p)
+{
+    if (!h || !p) return MM_ERR_INVALID;
+    *p = h->p;
+    return MM_OK;
+}
+
+int mm_padded_size(const mm_handle *h, int *n)
+{
+    if (!h || !n) return MM_ERR_INVALID;
+    *n = h->N;
+    return MM_OK;
+}
+
+void *mm_stream(mm_handle *h) { return h ? (void *)h->stream : nullptr; }
+
+int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int format,
+                      void *hip_stream)
+{
+    if (!h || !in || !out || count < 0) return MM_ERR_INVALID;
+    if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
+    if (count == 0) return MM_OK;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    HIPCHK(hipSetDevice(h->device));
+    return do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
+}
+
+int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, void *hip_stream)
+{
+    if (!h || !in || !out) return MM_ERR_INVALID;
+    if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
+    if (flags & MM_FRAMES_ON_DEVICE) return mm_process_stream(h, in, out, 1, format, hip_stream);
+    // host frames: stage through device buffers and synchronise
+    const size_t fb = (size_t)h->W * h->H * (format ? 16 : 4);
+    HIPCHK(hipSetDevice(h->device));
+    if (h->stage_bytes < fb) {
+        (void)hipFree(h->d_stage_in);
+        (void)hipFree(h->d_stage_out);
+        h->d_stage_in = h->d_stage_out = nullptr;
+        h->stage_bytes = 0;
+        if (hipMalloc(&h->d_stage_in, fb) != hipSuccess || hipMalloc(&h->d_stage_out, fb) != hipSuccess)
+            return MM_ERR_OOM;
+        h->stage_bytes = fb;
+    }
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    HIPCHK(hipMemcpyAsync(h->d_stage_in, in, fb, hipMemcpyHostToDevice, s));
+    int rc = do_stream(h, h->d_stage_in, h->d_stage_out, 1, format, s);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out, h->d_stage_out, fb, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MM_OK;
+}
+
+int mm_reset(mm_handle *h)
+{
+    if (!h) return MM_ERR_INVALID;
+    h->has_state = false;
+    return MM_OK;
+}
+
+int mm_state_size(const mm_handle *h, size_t *bytes)
+{
+    if (!h || !bytes) return MM_ERR_INVALID;
+    *bytes = sizeof(c2) * (size_t)(h->N / 2 + 1) * h->N;
+    return MM_OK;
+}
+
+int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
+{
+    size_t need = 0;
+    if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
+    if (!h->has_state) return MM_ERR_NO_STATE;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    HIPCHK(hipMemcpyAsync(dev_buf, h->d_state, need, hipMemcpyDeviceToDevice, s));
+    return MM_OK;
+}
+
+int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stream)
+{
+    size_t need = 0;
+    if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    HIPCHK(hipMemcpyAsync(h->d_state, dev_buf, need, hipMemcpyDeviceToDevice, s));
+    h->has_state = true;
+    return MM_OK;
+}
+
+int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf, size_t bytes,
+                     void *hip_stream)
+{
+    size_t need = 0;
+    if (!h || !in_dev || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
+    if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    HIPCHK(hipSetDevice(h->device));
+    return do_compute_state(h, (const uint8_t *)in_dev, format, (c2 *)dev_buf, s);
+}
+
+void mm_destroy(mm_handle *h)
+{
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    free_handle(h);
+}
+
+int mm_synth_frames(void *dev_out, int width, int height, int t0, int count, uint64_t seed,
+                    int gray, void *hip_stream)
+{
+    if (!dev_out || width <= 0 || height <= 0 || count <= 0) return MM_ERR_INVALID;
+    hipStream_t s = (hipStream_t)hip_stream;
+    hipLaunchKernelGGL(k_synth, dim3(4096), dim3(256), 0, s, (uint8_t *)dev_out, width, height,
+                       t0, count, seed, gray);
+    HIPCHK(hipGetLastError());
+    return MM_OK;
+}
+
+}  // extern "C"

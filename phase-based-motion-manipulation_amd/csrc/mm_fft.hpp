@@ -1,0 +1,144 @@
+// mm_fft.hpp — register/LDS Stockham FFT for one length-N complex sequence per
+// "FFT group" of T = N/8 threads (gfx950, wave64).
+//
+// Replaces the reference's per-stage radix-2 dispatches (FFT.compute:213-276,
+// driven 11+11 times per 2D FFT from MotionMagnificationProcessor.cs:522-549)
+// with log8(N) register passes and LDS exchanges inside one kernel.
+//
+// Layout contract ("L0"): thread t of the group holds v[j] = x[t + j*T],
+// j = 0..7, both before and after fft_regs<>().  A pass of radix R processes
+// B = 8/R butterflies per thread; butterfly b = t + q*T reads x[b + m*N/R]
+// (= register q + m*B) and, Stockham-style, writes y[(b/Ns)*Ns*R + b%Ns + m*Ns].
+// After the last pass (Ns*R == N) that index is t + (q+m*B)*T, i.e. register
+// q + m*B again, so the result stays in registers with no final LDS trip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mm {
+
+struct c2 { float x, y; };
+
+__device__ __forceinline__ c2 mk(float x, float y) { c2 r; r.x = x; r.y = y; return r; }
+__device__ __forceinline__ c2 add(c2 a, c2 b) { return mk(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ c2 sub(c2 a, c2 b) { return mk(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ c2 mul(c2 a, c2 b)
+{
+    return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ c2 scale(c2 a, float s) { return mk(a.x * s, a.y * s); }
+// multiply by i*DIR  (DIR = -1 forward -> -i ; DIR = +1 inverse -> +i)
+template <int DIR>
+__device__ __forceinline__ c2 mul_i(c2 a)
+{
+    return DIR < 0 ? mk(a.y, -a.x) : mk(-a.y, a.x);
+}
+
+// LDS index padding: one complex every 8 (bank-conflict-free Stockham writes
+// for Ns = 1 and Ns = 8 with ds_write_b64).
+__device__ __forceinline__ int pad8(int i) { return i + (i >> 3); }
+template <int N> constexpr int lds_complex() { return N + N / 8; }
+
+template <int DIR>
+__device__ __forceinline__ void dft2(c2 &a, c2 &b)
+{
+    c2 t = a;
+    a = add(t, b);
+    b = sub(t, b);
+}
+
+template <int DIR>
+__device__ __forceinline__ void dft4(c2 &x0, c2 &x1, c2 &x2, c2 &x3)
+{
+    c2 s0 = add(x0, x2), d0 = sub(x0, x2);
+    c2 s1 = add(x1, x3), d1 = mul_i<DIR>(sub(x1, x3));
+    x0 = add(s0, s1);
+    x2 = sub(s0, s1);
+    x1 = add(d0, d1);
+    x3 = sub(d0, d1);
+}
+
+template <int DIR>
+__device__ __forceinline__ void dft8(c2 *v)
+{
+    const float h = 0.70710678118654752f;
+    c2 a0 = add(v[0], v[4]), b0 = sub(v[0], v[4]);
+    c2 a1 = add(v[1], v[5]), b1 = sub(v[1], v[5]);
+    c2 a2 = add(v[2], v[6]), b2 = sub(v[2], v[6]);
+    c2 a3 = add(v[3], v[7]), b3 = sub(v[3], v[7]);
+    // b[n] *= W8^n, W8 = exp(DIR*i*pi/4)
+    b1 = mk(h * (b1.x - DIR * b1.y), h * (b1.y + DIR * b1.x));
+    b2 = mul_i<DIR>(b2);
+    b3 = mk(h * (-b3.x - DIR * b3.y), h * (-b3.y + DIR * b3.x));
+    dft4<DIR>(a0, a1, a2, a3);
+    dft4<DIR>(b0, b1, b2, b3);
+    v[0] = a0; v[2] = a1; v[4] = a2; v[6] = a3;
+    v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
+}
+
+// Twiddle W_N^idx from the device table tw[idx] = exp(-2*pi*i*idx/N).
+template <int DIR>
+__device__ __forceinline__ c2 twiddle(const c2 *__restrict__ tw, int idx)
+{
+    c2 w = tw[idx];
+    return DIR < 0 ? w : mk(w.x, -w.y);
+}
+
+template <int N, int R, int NS, int DIR, bool LAST>
+__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
+{
+    constexpr int T = N / 8;
+    constexpr int B = 8 / R;
+    constexpr int TWS = N / (NS * R);  // twiddle-table stride for W_{NS*R}
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+        const int b = t + q * T;
+        const int k = b & (NS - 1);
+        c2 u[R];
+#pragma unroll
+        for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
+        if (NS > 1) {
+#pragma unroll
+            for (int m = 1; m < R; ++m) u[m] = mul(u[m], twiddle<DIR>(tw, m * k * TWS));
+        }
+        if (R == 8) dft8<DIR>(u);
+        else if (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
+        else dft2<DIR>(u[0], u[1]);
+        if (LAST) {
+#pragma unroll
+            for (int m = 0; m < R; ++m) v[q + m * B] = u[m];
+        } else {
+            const int base = (b / NS) * NS * R + k;
+#pragma unroll
+            for (int m = 0; m < R; ++m) lds[pad8(base + m * NS)] = u[m];
+        }
+    }
+    if (!LAST) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = lds[pad8(t + j * T)];
+        __syncthreads();
+    }
+}
+
+template <int LOG2N, int DIR, int P, int NS>
+__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
+{
+    constexpr int R8 = LOG2N / 3;
+    constexpr int REM = LOG2N % 3;
+    constexpr int NP = R8 + (REM ? 1 : 0);
+    if constexpr (P < NP) {
+        constexpr int R = (P < R8) ? 8 : (REM == 2 ? 4 : 2);
+        fft_pass<(1 << LOG2N), R, NS, DIR, P == NP - 1>(v, t, lds, tw);
+        fft_pass_loop<LOG2N, DIR, P + 1, NS * R>(v, t, lds, tw);
+    }
+}
+
+// Unnormalised DFT of the group's sequence, DIR=-1 forward, DIR=+1 inverse.
+// Every thread of the WORKGROUP must call this (it contains __syncthreads).
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
+{
+    fft_pass_loop<LOG2N, DIR, 0, 1>(v, t, lds, tw);
+}
+
+}  // namespace mm

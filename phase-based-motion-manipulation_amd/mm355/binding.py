@@ -1,0 +1,198 @@
+"""ctypes binding of include/mm.h (lib/libmm355.so)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_ROOT = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmm355.so")
+HEADER = os.path.join(REPO_ROOT, "include", "mm.h")
+
+RGBA8 = 0
+RGBA32F = 1
+EDGE_REPEAT = 0
+EDGE_CLAMP = 1
+MODE_PYRAMID = 0
+FRAMES_ON_DEVICE = 1
+
+ERRORS = {0: "MM_OK", -1: "MM_ERR_INVALID", -2: "MM_ERR_UNSUPPORTED", -3: "MM_ERR_HIP",
+          -4: "MM_ERR_NO_DEVICE", -5: "MM_ERR_OOM", -6: "MM_ERR_NO_STATE"}
+
+
+class MMError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        name = ERRORS.get(code, str(code))
+        super().__init__(f"{what}: {name} ({strerror(code) if _lib else ''})")
+
+
+class Params(ctypes.Structure):
+    """mm_params — the inspector fields of the reference (.cs:12-31)."""
+    _fields_ = [("levels", ctypes.c_int), ("min_freq", ctypes.c_float),
+                ("max_freq", ctypes.c_float), ("phase_scale", ctypes.c_float),
+                ("magnitude_threshold", ctypes.c_float), ("orientations", ctypes.c_int),
+                ("mode", ctypes.c_int), ("edge_mode", ctypes.c_int),
+                ("apply_magnification", ctypes.c_int)]
+
+    @classmethod
+    def make(cls, levels=5, min_freq=0.05, max_freq=0.45, phase_scale=10.0,
+             magnitude_threshold=0.01, edge_mode=EDGE_REPEAT, apply_magnification=True):
+        p = cls()
+        lib().mm_params_default(ctypes.byref(p))
+        p.levels, p.min_freq, p.max_freq = levels, min_freq, max_freq
+        p.phase_scale, p.magnitude_threshold = phase_scale, magnitude_threshold
+        p.edge_mode, p.apply_magnification = edge_mode, 1 if apply_magnification else 0
+        return p
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load the HIP product library; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise MMError(-3, f"HIP library not built: {path} (run __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    vp, ci, cf, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    pp = ctypes.POINTER(Params)
+    sigs = {
+        "mm_abi_version": (ci, []),
+        "mm_strerror": (ctypes.c_char_p, [ci]),
+        "mm_params_default": (ci, [pp]),
+        "mm_create": (ci, [ci, ci, pp, ci, ctypes.POINTER(vp)]),
+        "mm_set_params": (ci, [vp, pp]),
+        "mm_get_params": (ci, [vp, pp]),
+        "mm_padded_size": (ci, [vp, ctypes.POINTER(ci)]),
+        "mm_process": (ci, [vp, vp, vp, ci, ci, vp]),
+        "mm_process_stream": (ci, [vp, vp, vp, ci, ci, vp]),
+        "mm_reset": (ci, [vp]),
+        "mm_state_size": (ci, [vp, ctypes.POINTER(sz)]),
+        "mm_get_state": (ci, [vp, vp, sz, vp]),
+        "mm_set_state": (ci, [vp, vp, sz, vp]),
+        "mm_compute_state": (ci, [vp, vp, ci, vp, sz, vp]),
+        "mm_stream": (vp, [vp]),
+        "mm_destroy": (None, [vp]),
+        "mm_synth_frames": (ci, [vp, ci, ci, ci, ci, ctypes.c_uint64, ci, vp]),
+        "mm_resample_table": (ci, [ci, ci, ci, ci, ctypes.POINTER(ctypes.c_int32),
+                                   ctypes.POINTER(cf)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def lib():
+    return load_library()
+
+
+def strerror(code):
+    return lib().mm_strerror(code).decode()
+
+
+def check(rc, what):
+    if rc != 0:
+        raise MMError(rc, what)
+
+
+def abi_symbols():
+    """Function names declared in include/mm.h."""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mm_[a-z_0-9]+)\s*\(", txt)))
+
+
+def resample_table(width, height, axis, edge_mode=EDGE_REPEAT):
+    n = width if axis == 0 else height
+    idx = np.zeros((n, 4), np.int32)
+    w = np.zeros((n, 4), np.float32)
+    check(lib().mm_resample_table(width, height, axis, edge_mode,
+                                  idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                  w.ctypes.data_as(ctypes.POINTER(ctypes.c_float))),
+          "mm_resample_table")
+    return idx, w
+
+
+def _ptr(x):
+    """Device/host address of a torch tensor, numpy array or int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(f"cannot take the address of {type(x)}")
+
+
+class Handle:
+    """One mm_handle (one video stream on one GPU)."""
+
+    def __init__(self, width, height, params=None, device=0):
+        self.width, self.height = width, height
+        self.params = params if params is not None else Params.make()
+        h = ctypes.c_void_p()
+        check(lib().mm_create(width, height, ctypes.byref(self.params), device, ctypes.byref(h)),
+              "mm_create")
+        self.h = h
+        n = ctypes.c_int()
+        check(lib().mm_padded_size(self.h, ctypes.byref(n)), "mm_padded_size")
+        self.N = n.value
+        s = ctypes.c_size_t()
+        check(lib().mm_state_size(self.h, ctypes.byref(s)), "mm_state_size")
+        self.state_bytes = s.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib().mm_stream(self.h)
+
+    def set_params(self, params):
+        self.params = params
+        check(lib().mm_set_params(self.h, ctypes.byref(params)), "mm_set_params")
+
+    def process(self, src, dst, fmt, on_device=True, stream=None):
+        check(lib().mm_process(self.h, _ptr(src), _ptr(dst), fmt,
+                               FRAMES_ON_DEVICE if on_device else 0, _ptr(stream)),
+              "mm_process")
+
+    def process_stream(self, src, dst, count, fmt, stream=None):
+        check(lib().mm_process_stream(self.h, _ptr(src), _ptr(dst), count, fmt, _ptr(stream)),
+              "mm_process_stream")
+
+    def reset(self):
+        check(lib().mm_reset(self.h), "mm_reset")
+
+    def get_state(self, dev_buf, stream=None):
+        check(lib().mm_get_state(self.h, _ptr(dev_buf), self.state_bytes, _ptr(stream)),
+              "mm_get_state")
+
+    def set_state(self, dev_buf, stream=None):
+        check(lib().mm_set_state(self.h, _ptr(dev_buf), self.state_bytes, _ptr(stream)),
+              "mm_set_state")
+
+    def compute_state(self, src, fmt, dev_buf, stream=None):
+        check(lib().mm_compute_state(self.h, _ptr(src), fmt, _ptr(dev_buf), self.state_bytes,
+                                     _ptr(stream)), "mm_compute_state")
+
+    def synth(self, dev_out, t0, count, seed=0x5EED0000, gray=False, stream=None):
+        check(lib().mm_synth_frames(_ptr(dev_out), self.width, self.height, t0, count, seed,
+                                    1 if gray else 0, _ptr(stream)), "mm_synth_frames")

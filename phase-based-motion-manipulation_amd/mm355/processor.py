@@ -1,0 +1,114 @@
+"""Mirror of the reference Unity component ``MotionMagnificationProcessor``
+(Assets/Scripts/MotionMagnificationProcessor.cs) on top of the C-ABI.
+
+Field names follow the reference's serialized inspector fields (.cs:7-43) in
+snake_case; methods keep the reference's Unity callback names.
+"""
+import numpy as np
+
+from .binding import (EDGE_REPEAT, RGBA8, RGBA32F, Handle, MMError, Params)
+
+
+def _fmt_of(frame):
+    dt = str(getattr(frame, "dtype", ""))
+    if dt.endswith("uint8"):
+        return RGBA8
+    if dt.endswith("float32"):
+        return RGBA32F
+    raise MMError(-1, f"frame dtype {dt} (want uint8 or float32 RGBA)")
+
+
+def _is_device(frame):
+    return bool(getattr(frame, "is_cuda", False))
+
+
+class MotionMagnificationProcessor:
+    """[RequireComponent(typeof(Camera))] class MotionMagnificationProcessor (.cs:4-5).
+
+    ``width``/``height`` play the role of Screen.width/height read in
+    InitializeProcessor (.cs:298-299): geometry is frozen at Start().
+    """
+
+    def __init__(self, width, height, *, apply_motion_magnification=True,
+                 show_magnitude=False, show_phase=False, use_pyramid_decomposition=True,
+                 pyramid_levels=5, min_frequency=0.05, max_frequency=0.45,
+                 phase_scale=10.0, magnitude_threshold=0.01, edge_mode=EDGE_REPEAT,
+                 device=0):
+        self.width, self.height, self.device = width, height, device
+        self.apply_motion_magnification = apply_motion_magnification  # .cs:12
+        self.show_magnitude = show_magnitude                          # .cs:13
+        self.show_phase = show_phase                                  # .cs:14
+        self.use_pyramid_decomposition = use_pyramid_decomposition    # .cs:18
+        self.pyramid_levels = pyramid_levels                          # .cs:19
+        self.min_frequency = min_frequency                            # .cs:20
+        self.max_frequency = max_frequency                            # .cs:21
+        self.phase_scale = phase_scale                                # .cs:29
+        self.magnitude_threshold = magnitude_threshold                # .cs:30
+        self.edge_mode = edge_mode
+        self._handle = None
+
+    # -- reference lifecycle -------------------------------------------------
+    def _params(self):
+        if not self.use_pyramid_decomposition:
+            # ProcessFrameWithStandardMagnification (.cs:208-232): not built yet
+            raise MMError(-2, "use_pyramid_decomposition=False (standard mode)")
+        if self.show_magnitude or self.show_phase:
+            raise MMError(-2, "debug views (.cs:234-257) are out of scope")
+        return Params.make(levels=self.pyramid_levels, min_freq=self.min_frequency,
+                           max_freq=self.max_frequency, phase_scale=self.phase_scale,
+                           magnitude_threshold=self.magnitude_threshold,
+                           edge_mode=self.edge_mode,
+                           apply_magnification=self.apply_motion_magnification)
+
+    def Start(self):
+        """Start -> InitializeProcessor (.cs:90-94, :289-342). Raises on failure."""
+        self._handle = Handle(self.width, self.height, self._params(), self.device)
+        return self
+
+    def OnValidate(self):
+        """OnValidate (.cs:78-88): push edited fields; effective next frame."""
+        if self._handle is not None:
+            self._handle.set_params(self._params())
+
+    def OnRenderImage(self, source, destination):
+        """OnRenderImage (.cs:101-143). source/destination: [H, W, 4] uint8 or
+        float32, both torch CUDA tensors (async on the handle's stream) or both
+        host numpy arrays (synchronous)."""
+        if self._handle is None:                       # !isInitialized -> Blit (.cs:103-107)
+            destination[...] = source
+            return
+        fmt = _fmt_of(source)
+        if _fmt_of(destination) != fmt:
+            raise MMError(-1, "source/destination formats differ")
+        on_dev = _is_device(source)
+        if on_dev != _is_device(destination):
+            raise MMError(-1, "source and destination must both be device or host")
+        if not on_dev:
+            if not (source.flags.c_contiguous and destination.flags.c_contiguous):
+                raise MMError(-1, "frames must be C-contiguous")
+        elif not (source.is_contiguous() and destination.is_contiguous()):
+            raise MMError(-1, "frames must be contiguous")
+        self._handle.process(source, destination, fmt, on_device=on_dev)
+
+    def OnDestroy(self):
+        """OnDestroy -> ReleaseResources (.cs:96-99, :344-356)."""
+        if self._handle is not None:
+            self._handle.close()
+            self._handle = None
+
+    # -- extras ---------------------------------------------------------------
+    def reset(self):
+        """isFirstFrame = true (.cs:75): next frame passes through."""
+        self._handle.reset()
+
+    @property
+    def handle(self):
+        return self._handle
+
+    @property
+    def padded_size(self):
+        return self._handle.N if self._handle else None
+
+
+def host_frames(n, h, w, fmt):
+    return np.zeros((n, h, w, 4), np.uint8 if fmt == RGBA8 else np.float32)

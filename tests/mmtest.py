@@ -1,0 +1,72 @@
+"""Shared helpers for the GPU parity tests (HIP path through the C-ABI)."""
+import numpy as np
+
+import oracle_py as O
+
+# Tolerances, RGB in [0, 1]:
+TOL_MAX = 1e-4      # max-abs, fp32 HIP vs fp32 oracle, integer phase scale
+TOL_RMSE = 1e-5     # RMSE
+TOL_P999 = 1e-4     # 99.9th percentile, non-integer phase scale (wrap ties at |d|~pi)
+U8_FRAC = 1e-3      # RGBA8: exact except +-1 LSB on <= 0.1% of values
+
+
+def synth(W, H, n, t0=0, gray=False, seed=0x5EED0000, fmt="f32"):
+    fr = [O.synth_frame(W, H, t0 + t, seed=seed, gray=gray) for t in range(n)]
+    if fmt == "u8":
+        return fr
+    return [f.astype(np.float32) / np.float32(255.0) for f in fr]
+
+
+def oracle_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, apply=True):
+    o = O.Oracle(W, H, levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
+                 edge_mode=edge)
+    o.set_apply(apply)
+    return [o.process(f) for f in frames]
+
+
+def gpu_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, mode="frame",
+            apply=True):
+    import torch
+    import mm355
+    p = mm355.Params.make(levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
+                          edge_mode=edge, apply_magnification=apply)
+    h = mm355.Handle(W, H, p)
+    fmt = mm355.RGBA8 if frames[0].dtype == np.uint8 else mm355.RGBA32F
+    dev_in = torch.from_numpy(np.stack(frames)).cuda()
+    dev_out = torch.empty_like(dev_in)
+    if mode == "frame":
+        for k in range(len(frames)):
+            h.process(dev_in[k], dev_out[k], fmt)
+    elif mode == "stream":
+        h.process_stream(dev_in, dev_out, len(frames), fmt)
+    elif mode == "host":
+        outs = []
+        for f in frames:
+            o = np.empty_like(f)
+            h.process(f, o, fmt, on_device=False)
+            outs.append(o)
+        h.close()
+        return outs
+    torch.cuda.synchronize()
+    res = dev_out.cpu().numpy()
+    h.close()
+    return list(res)
+
+
+def err_stats(a, b):
+    e = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    return e.max(), float(np.sqrt((e ** 2).mean())), float(np.quantile(e, 0.999))
+
+
+def assert_close_f32(gpu, ref, integer_scale=True):
+    mx, rmse, p999 = err_stats(gpu, ref)
+    if integer_scale:
+        assert mx <= TOL_MAX and rmse <= TOL_RMSE, (mx, rmse, p999)
+    else:
+        assert p999 <= TOL_P999 and rmse <= TOL_RMSE * 10, (mx, rmse, p999)
+
+
+def assert_close_u8(gpu, ref):
+    d = np.abs(gpu.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() <= 1, d.max()
+    assert (d > 0).mean() <= U8_FRAC, (d > 0).mean()

@@ -1,0 +1,172 @@
+"""HIP path (through the C-ABI) vs the CPU oracle on the same seeded inputs.
+
+Bars: fp32 max-abs <= 1e-4 and RMSE <= 1e-5 at integer phase
+scale; 99.9th percentile <= 1e-4 at non-integer scale; RGBA8 exact except
++-1 LSB on <= 0.1% of values; first frame bitwise.
+"""
+import numpy as np
+import pytest
+
+import mmtest as T
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("W,H,L,S,edge", [
+    (64, 48, 5, 10.0, 0), (64, 48, 4, 25.0, 0), (64, 48, 6, 25.0, 1), (64, 48, 5, 9.7, 0),
+    (128, 96, 5, 25.0, 0), (200, 120, 5, 25.0, 1), (96, 96, 2, 10.0, 0), (64, 64, 1, 10.0, 1)])
+def test_small_f32(W, H, L, S, edge):
+    fr = T.synth(W, H, 4)
+    ref = T.oracle_run(W, H, fr, L, S, edge)
+    got = T.gpu_run(W, H, fr, L, S, edge)
+    assert np.array_equal(got[0], fr[0])                   # first frame passthrough
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r, integer_scale=float(S).is_integer())
+        assert np.all(g[..., 3] == 1.0)
+
+
+def test_c1_256_gray_L3():
+    """BASELINE config 0: 256x256 gray, 3 levels, PhaseScale 10, 32 frames."""
+    fr = T.synth(256, 256, 32, gray=True)
+    ref = T.oracle_run(256, 256, fr, 3, 10.0)
+    got = T.gpu_run(256, 256, fr, 3, 10.0, mode="stream")
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r)
+
+
+def test_u8_frames():
+    W, H = 128, 96
+    fr = T.synth(W, H, 5, fmt="u8")
+    ref = T.oracle_run(W, H, fr, 5, 25.0)
+    got = T.gpu_run(W, H, fr, 5, 25.0)
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_u8(g, r)
+
+
+def test_stream_equals_per_frame_bitwise():
+    W, H = 200, 120
+    fr = T.synth(W, H, 19)                  # crosses the 8-frame chunk boundary twice
+    a = T.gpu_run(W, H, fr, 5, 25.0, mode="frame")
+    b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream")
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_host_pointer_path():
+    W, H = 64, 48
+    fr = T.synth(W, H, 3)
+    a = T.gpu_run(W, H, fr, 5, 10.0, mode="host")
+    b = T.gpu_run(W, H, fr, 5, 10.0, mode="frame")
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_apply_off_passthrough_and_state():
+    W, H = 64, 48
+    fr = T.synth(W, H, 3)
+    got = T.gpu_run(W, H, fr, 5, 10.0, apply=False)
+    for g, f in zip(got, fr):
+        assert np.array_equal(g, f)
+
+
+def test_forward_spectrum_matches_oracle():
+    """K1+K2 forward path alone: mm_compute_state vs the oracle's F_t."""
+    import torch
+    import mm355
+    W, H = 128, 96
+    f0, f1 = T.synth(W, H, 2)
+    o = O.Oracle(W, H)
+    o.process(f0)
+    _, dbg = o.process(f1, dbg=True)
+    Fc = dbg["F_cur"]
+    h = mm355.Handle(W, H)
+    N = h.N
+    st = torch.empty(h.state_bytes, dtype=torch.uint8, device="cuda")
+    h.compute_state(torch.from_numpy(f1).cuda(), mm355.RGBA32F, st)
+    torch.cuda.synchronize()
+    half = st.view(torch.float32).cpu().numpy().reshape(N // 2 + 1, N, 2)
+    half = half[..., 0] + 1j * half[..., 1]
+    fx = np.arange(N // 2 + 1)
+    fy = np.arange(N)
+    ref = Fc[((fy + N // 2) % N)[None, :], ((fx + N // 2) % N)[:, None]]
+    assert np.abs(half - ref).max() / np.abs(ref).max() < 2e-6
+    h.close()
+
+
+def test_state_get_set_and_reset():
+    import torch
+    import mm355
+    W, H = 64, 48
+    fr = T.synth(W, H, 4)
+    full = T.gpu_run(W, H, fr, 5, 25.0)
+    p = mm355.Params.make(phase_scale=25.0)
+    a = mm355.Handle(W, H, p)
+    b = mm355.Handle(W, H, p)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    out = torch.empty_like(dev)
+    a.process(dev[0], out[0], mm355.RGBA32F)
+    a.process(dev[1], out[1], mm355.RGBA32F)
+    st = torch.empty(a.state_bytes, dtype=torch.uint8, device="cuda")
+    a.get_state(st)
+    torch.cuda.synchronize()
+    b.set_state(st)
+    b.process(dev[2], out[2], mm355.RGBA32F)
+    torch.cuda.synchronize()
+    assert np.array_equal(out[2].cpu().numpy(), full[2])
+    b.reset()
+    b.process(dev[3], out[3], mm355.RGBA32F)
+    torch.cuda.synchronize()
+    assert np.array_equal(out[3].cpu().numpy(), fr[3])   # passthrough after reset
+    with pytest.raises(mm355.MMError):
+        mm355.Handle(W, H).get_state(st)                 # MM_ERR_NO_STATE
+    a.close()
+    b.close()
+
+
+def test_processor_mirror():
+    import torch
+    import mm355
+    W, H = 64, 48
+    fr = T.synth(W, H, 3)
+    ref = T.oracle_run(W, H, fr, 5, 25.0)
+    proc = mm355.MotionMagnificationProcessor(W, H, phase_scale=1.0).Start()
+    proc.phase_scale = 25.0
+    proc.OnValidate()
+    src = torch.from_numpy(np.stack(fr)).cuda()
+    dst = torch.empty_like(src)
+    for k in range(3):
+        proc.OnRenderImage(src[k], dst[k])
+    torch.cuda.synchronize()
+    for k in range(1, 3):
+        T.assert_close_f32(dst[k].cpu().numpy(), ref[k])
+    proc.OnDestroy()
+
+
+@pytest.mark.slow
+def test_c2_1080p_vs_oracle():
+    """BASELINE config 1 geometry: 1920x1080 RGBA, L=5, PhaseScale=25."""
+    W, H = 1920, 1080
+    fr = T.synth(W, H, 3, fmt="u8")
+    ref = T.oracle_run(W, H, fr, 5, 25.0)
+    got = T.gpu_run(W, H, fr, 5, 25.0, mode="stream")
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_u8(g, r)
+    ff = [f.astype(np.float32) / np.float32(255) for f in fr[:2]]
+    rf = T.oracle_run(W, H, ff, 5, 25.0)
+    gf = T.gpu_run(W, H, ff, 5, 25.0)
+    T.assert_close_f32(gf[1], rf[1])
+
+
+@pytest.mark.slow
+def test_c3_2160p_vs_oracle():
+    """BASELINE config 2 geometry: 3840x2160 RGBA, L=6, PhaseScale=25."""
+    W, H = 3840, 2160
+    ff = T.synth(W, H, 2)
+    rf = T.oracle_run(W, H, ff, 6, 25.0)
+    gf = T.gpu_run(W, H, ff, 6, 25.0)
+    assert np.array_equal(gf[0], ff[0])
+    T.assert_close_f32(gf[1], rf[1])
