@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py — magnified frames/s of the MI355X-native MotionMagnificationProcessor.
+
+Workload (BASELINE.json configs[1]): a synthetic 1920x1080 RGBA8 stream,
+5-level pyramid, PhaseScale 25, pyramid mode with orientations = 1 (the
+reference's semantics).  One STEP = one pass of the hot path over one batch of
+`--frames-per-step` consecutive frames of the stream per GPU (default 30, so
+the default 10 timed steps are the 300-frame stream of the config).  Input
+frames are generated on the device and resident in HBM before timing.
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): the stream is
+frame-sharded: each step rank g processes its own contiguous
+chunk and one RCCL ring shift carries the chunk-boundary temporal state
+(`--mode ring`, default).  `--mode replicas` runs independent streams
+(BASELINE configs[4]).  Weak scaling either way.
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with
+`roofline` (dominant kernel, HIP-event time measured on its launch stream
+inside the timed region) and `cpu_baseline` (the oracle on host cores, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "phase-based-motion-manipulation_amd"))
+
+METRIC = ("magnified frames/sec at 1920×1080, 5-level pyramid; "
+          "achieved HBM GB/s vs peak")
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(W, H, N, b_in=4, b_out=4):
+    """B = W*H*(2*b_in + b_out) + 6*N^2*8 per output frame,
+    split over the three kernels as they move it."""
+    nn8 = N * N * 8
+    return {"k_rows_fwd": W * H * b_in + nn8,            # read frame, write row->col handoff
+            "k_cols": 4 * nn8,                          # handoff in/out + state in/out
+            "k_rows_inv": nn8 + W * H * (b_in + b_out),  # handoff in, frame in (I/Q), frame out
+            "frame": W * H * (2 * b_in + b_out) + 6 * nn8}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames-per-step", type=int, default=30)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--levels", type=int, default=5)
+    ap.add_argument("--phase-scale", type=float, default=25.0)
+    ap.add_argument("--mode", choices=("ring", "replicas"), default="ring")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="bound on the CPU-baseline sample")
+    return ap.parse_args()
+
+
+class GpuBackend:
+    """ShardedStream backend over one mm355 handle; frames pre-generated."""
+
+    def __init__(self, handle, frames, out, fmt, chunk, world, rank, torch):
+        self.h, self.frames, self.out, self.fmt = handle, frames, out, fmt
+        self.chunk, self.world, self.rank, self.torch = chunk, world, rank, torch
+
+    def _stream(self):
+        return self.torch.cuda.current_stream().cuda_stream
+
+    def _local(self, frame_index):
+        step = frame_index // (self.world * self.chunk)
+        return step, frame_index - step * self.world * self.chunk - self.rank * self.chunk
+
+    def empty_state(self):
+        return self.torch.empty(self.h.state_bytes, dtype=self.torch.uint8, device="cuda")
+
+    def state_of(self, frame_index):
+        s, k = self._local(frame_index)
+        buf = self.empty_state()
+        self.h.compute_state(self.frames[s % len(self.frames), k], self.fmt, buf,
+                             stream=self._stream())
+        return buf
+
+    def set_state(self, buf):
+        self.h.set_state(buf, stream=self._stream())
+
+    def reset(self):
+        self.h.reset()
+
+    def process(self, lo, count):
+        s, k = self._local(lo)
+        self.h.process_stream(self.frames[s % len(self.frames), k], self.out, count, self.fmt,
+                              stream=self._stream())
+
+
+def cpu_baseline(W, H, L, S, seconds):
+    """The CPU oracle (literal restatement of the reference algorithm) on the
+    host cores, bounded sample of the same stream."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = O.set_threads(threads)
+    o = O.Oracle(W, H, levels=L, phase_scale=S)
+    o.process(O.synth_frame(W, H, 0))          # first frame: passthrough, excluded
+    n, t0 = 0, time.perf_counter()
+    while n < 30:
+        o.process(O.synth_frame(W, H, n + 1))
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frames (t=1..{n}) of the same {W}x{H} synthetic stream, "
+                      f"L={L}, S={S}, after the passthrough frame; literal fp32 C "
+                      f"restatement (radix-2, 2 forward FFTs/frame), OpenMP {threads} threads"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import mm355
+    from mm355.stream import ShardedStream
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    W, H, C = a.width, a.height, a.frames_per_step
+    os.environ.setdefault("MM_CHUNK", str(C))
+    params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale)
+    h = mm355.Handle(W, H, params, device=local)
+    N = h.N
+
+    # resident inputs: one buffer per step (warmup + timed), generated on device
+    total_steps = a.warmup + a.steps
+    ring = a.mode == "ring" and world > 1
+    seed = 0x5EED0000 + (0 if a.mode == "ring" else rank)
+    frames = torch.empty((total_steps, C, H, W, 4), dtype=torch.uint8, device="cuda")
+    for s in range(total_steps):
+        t0 = (s * world * C + rank * C) if a.mode == "ring" else s * C
+        h.synth(frames[s], t0, C, seed=seed, stream=torch.cuda.current_stream().cuda_stream)
+    out = torch.empty((C, H, W, 4), dtype=torch.uint8, device="cuda")
+    backend = GpuBackend(h, frames, out, mm355.RGBA8, C, world if ring else 1,
+                         rank if ring else 0, torch)
+    stream = ShardedStream(backend, C, rank if ring else 0, world if ring else 1)
+    torch.cuda.synchronize()
+
+    for s in range(a.warmup):
+        stream.step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    h.profile_begin()
+    t_start = time.perf_counter()
+    for s in range(a.warmup, total_steps):
+        stream.step(s)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    prof = h.profile_end()
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_total = a.steps * C * world
+    fps = frames_total / elapsed
+    ab = algorithmic_bytes(W, H, N)
+    kern = {}
+    for name, (ms, launches, nfr) in prof.items():
+        if launches:
+            kern[name] = {"ms_total": round(ms, 4), "launches": launches, "frames": nfr,
+                          "ms_per_launch": round(ms / launches, 5),
+                          "algorithmic_bytes_per_launch": ab[name] * nfr / launches}
+    dom = max(kern, key=lambda k: kern[k]["ms_total"])
+    dk = kern[dom]
+    achieved = dk["algorithmic_bytes_per_launch"] / (dk["ms_per_launch"] * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("frames_per_launch") == C and dom in tj.get("kernels", {}):
+                traffic = tj["kernels"][dom]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
+                               f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)",
+                   "frames_per_step_per_gpu": C, "padded_n": N,
+                   "parallelism": (f"frame-sharded x{world}, RCCL ring state shift"
+                                   if ring else f"replicas x{world}")},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                     "traffic": traffic},
+        "frame_algorithmic_GBps": round(ab["frame"] * fps / world / 1e9, 2),
+        "kernels": kern,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(W, H, a.levels, a.phase_scale, a.cpu_seconds)
+    h.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

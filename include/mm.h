@@ -123,6 +123,18 @@ const char *mm_strerror(int code);
 int mm_abi_version(void);
 
 /* ---- utilities (not on the reference surface) ---- */
+/* Per-kernel device time, measured with HIP events recorded on the launch
+ * stream around every launch between mm_profile_begin and mm_profile_end.
+ * Kernel ids: */
+#define MM_K_ROWS_FWD 0   /* K1: resample + window + row real FFT      */
+#define MM_K_COLS     1   /* K2: column FFT + pyramid phase op + IFFT  */
+#define MM_K_ROWS_INV 2   /* K3: row C2R IFFT + blur + recombine + crop */
+#define MM_K_COUNT    3
+int mm_profile_begin(mm_handle *h);
+/* Waits for the recorded events; ms[k] = summed device ms, launches[k],
+ * frames[k] = frames processed by kernel k (any pointer may be NULL). */
+int mm_profile_end(mm_handle *h, double *ms, int *launches, int *frames);
+
 /* Synthetic stream frames generated on the device:
  * frames t0..t0+count-1 into dev_out (RGBA8). */
 int mm_synth_frames(void *dev_out, int width, int height, int t0, int count,

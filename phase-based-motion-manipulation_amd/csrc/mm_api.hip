@@ -49,6 +49,30 @@ struct mm_handle {
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
+    // mm_profile_begin/end: HIP events around each launch on its stream
+    struct ProfRec { hipEvent_t a, b; int kernel, frames; };
+    bool prof;
+    std::vector<ProfRec> prof_recs;
+};
+
+// Brackets one kernel launch with events when profiling is on.
+struct ProfScope {
+    mm_handle *h;
+    hipStream_t s;
+    mm_handle::ProfRec r;
+    bool on;
+    ProfScope(mm_handle *h_, hipStream_t s_, int kernel, int frames) : h(h_), s(s_), on(h_->prof)
+    {
+        if (!on) return;
+        r.kernel = kernel;
+        r.frames = frames;
+        on = hipEventCreate(&r.a) == hipSuccess && hipEventCreate(&r.b) == hipSuccess &&
+             hipEventRecord(r.a, s) == hipSuccess;
+    }
+    ~ProfScope()
+    {
+        if (on && hipEventRecord(r.b, s) == hipSuccess) h->prof_recs.push_back(r);
+    }
 };
 
 // ------------------------------------------------------------------------
@@ -189,6 +213,7 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
     const int gpw = groups_per_wg<LOG2N>();
     const int blocks = (total + gpw - 1) / gpw;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
     if (fmt == MM_RGBA8)
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(wg_threads<LOG2N>()),
                            lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col,
@@ -208,6 +233,7 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     const int gpw = groups_per_wg<LOG2N>();
     const int cols = (1 << LOG2N) / 2 + 1;
     const int blocks = (cols + gpw - 1) / gpw;
+    ProfScope ps(h, s, MM_K_COLS, nframes);
     hipLaunchKernelGGL((k_cols<LOG2N>), dim3(blocks), dim3(wg_threads<LOG2N>()),
                        lds_fft_bytes<LOG2N>(), s, h->d_G, h->g_stride, h->d_Q, h->q_stride,
                        st_in, st_out, nframes, first_passthrough, h->geo, h->spec, h->d_tw);
@@ -225,6 +251,7 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     const int bands = (h->H + br - 1) / br;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     const size_t lds = lds_k3_bytes<LOG2N>(h->W);
+    ProfScope ps(h, s, MM_K_ROWS_INV, nout);
     if (fmt == MM_RGBA8)
         hipLaunchKernelGGL((k_rows_inv<LOG2N, 0>), dim3(bands * nout), dim3(wg_threads<LOG2N>()),
                            lds, s, h->d_Q, h->q_stride, in, out, fb, frame0, bands, br, h->geo,
@@ -384,6 +411,10 @@ static void free_handle(mm_handle *h)
     (void)hipFree(h->d_stage_in);
     (void)hipFree(h->d_stage_out);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    for (auto &r : h->prof_recs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
     delete h;
 }
 
@@ -592,6 +623,44 @@ void mm_destroy(mm_handle *h)
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
     free_handle(h);
+}
+
+int mm_profile_begin(mm_handle *h)
+{
+    if (!h) return MM_ERR_INVALID;
+    for (auto &r : h->prof_recs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    h->prof_recs.clear();
+    h->prof = true;
+    return MM_OK;
+}
+
+int mm_profile_end(mm_handle *h, double *ms, int *launches, int *frames)
+{
+    if (!h) return MM_ERR_INVALID;
+    double t[MM_K_COUNT] = {0, 0, 0};
+    int n[MM_K_COUNT] = {0, 0, 0}, f[MM_K_COUNT] = {0, 0, 0};
+    int rc = MM_OK;
+    for (auto &r : h->prof_recs) {
+        float e = 0.0f;
+        if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&e, r.a, r.b) != hipSuccess)
+            rc = MM_ERR_HIP;
+        t[r.kernel] += e;
+        n[r.kernel] += 1;
+        f[r.kernel] += r.frames;
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    h->prof_recs.clear();
+    h->prof = false;
+    for (int k = 0; k < MM_K_COUNT; ++k) {
+        if (ms) ms[k] = t[k];
+        if (launches) launches[k] = n[k];
+        if (frames) frames[k] = f[k];
+    }
+    return rc;
 }
 
 int mm_synth_frames(void *dev_out, int width, int height, int t0, int count, uint64_t seed,

@@ -1,0 +1,113 @@
+/*
+ * mm_cli.c — C host driver over the C-ABI (include/mm.h).
+ *
+ * Plays the role of the Unity camera that calls OnRenderImage once per frame
+ * (Assets/Scripts/MotionMagnificationProcessor.cs:101): it generates a
+ * synthetic RGBA8 stream on the device, runs the magnifier over
+ * it and reports throughput.  Optional raw RGBA8 file I/O for real clips.
+ *
+ *   mm_cli [-w W] [-h H] [-n frames] [-l levels] [-s phase_scale]
+ *          [-b frames_per_call] [-i in.rgba] [-o out.rgba] [-d device]
+ */
+#include <hip/hip_runtime_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mm.h"
+
+#define CHECK(x)                                                                      \
+    do {                                                                              \
+        int rc_ = (x);                                                                \
+        if (rc_ != MM_OK) {                                                           \
+            fprintf(stderr, "%s failed: %s (%d)\n", #x, mm_strerror(rc_), rc_);       \
+            return 1;                                                                 \
+        }                                                                             \
+    } while (0)
+
+int main(int argc, char **argv)
+{
+    int W = 1920, H = 1080, F = 300, L = 5, B = 30, dev = 0;
+    float S = 25.0f;
+    const char *in_path = NULL, *out_path = NULL;
+    for (int i = 1; i < argc; ++i) {
+        const char *a = argv[i];
+        const char *v = i + 1 < argc ? argv[i + 1] : NULL;
+        if (!v) { fprintf(stderr, "missing value for %s\n", a); return 2; }
+        if (!strcmp(a, "-w")) W = atoi(v);
+        else if (!strcmp(a, "-h")) H = atoi(v);
+        else if (!strcmp(a, "-n")) F = atoi(v);
+        else if (!strcmp(a, "-l")) L = atoi(v);
+        else if (!strcmp(a, "-s")) S = (float)atof(v);
+        else if (!strcmp(a, "-b")) B = atoi(v);
+        else if (!strcmp(a, "-d")) dev = atoi(v);
+        else if (!strcmp(a, "-i")) in_path = v;
+        else if (!strcmp(a, "-o")) out_path = v;
+        else { fprintf(stderr, "unknown option %s\n", a); return 2; }
+        ++i;
+    }
+    if (B < 1) B = 1;
+    mm_params p;
+    mm_params_default(&p);
+    p.levels = L;
+    p.phase_scale = S;
+    mm_handle *h = NULL;
+    CHECK(mm_create(W, H, &p, dev, &h));
+    int N = 0;
+    mm_padded_size(h, &N);
+    printf("Original: %dx%d, Padded: %dx%d\n", W, H, N, N);   /* .cs:304 */
+
+    const size_t fb = (size_t)W * H * 4;
+    void *d_in = NULL, *d_out = NULL;
+    if (hipMalloc(&d_in, fb * B) != hipSuccess || hipMalloc(&d_out, fb * B) != hipSuccess) {
+        fprintf(stderr, "hipMalloc failed\n");
+        return 1;
+    }
+    hipStream_t s = (hipStream_t)mm_stream(h);
+    FILE *fi = in_path ? fopen(in_path, "rb") : NULL;
+    FILE *fo = out_path ? fopen(out_path, "wb") : NULL;
+    if ((in_path && !fi) || (out_path && !fo)) { fprintf(stderr, "cannot open file\n"); return 1; }
+    unsigned char *host = (fi || fo) ? (unsigned char *)malloc(fb * B) : NULL;
+
+    double t_proc = 0.0;
+    int done = 0;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    while (done < F) {
+        int n = F - done < B ? F - done : B;
+        if (fi) {
+            size_t got = fread(host, fb, (size_t)n, fi);
+            if (got == 0) break;
+            n = (int)got;
+            hipMemcpyAsync(d_in, host, fb * n, hipMemcpyHostToDevice, s);
+        } else {
+            CHECK(mm_synth_frames(d_in, W, H, done, n, 0x5EED0000ull, 0, s));
+        }
+        hipEventRecord(e0, s);
+        CHECK(mm_process_stream(h, d_in, d_out, n, MM_RGBA8, s));
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (done > 0) t_proc += ms * 1e-3;      /* first call holds the passthrough frame */
+        if (fo) {
+            hipMemcpy(host, d_out, fb * n, hipMemcpyDeviceToHost);
+            fwrite(host, fb, (size_t)n, fo);
+        }
+        done += n;
+    }
+    int timed = done - (done > B ? B : done);
+    if (timed > 0 && t_proc > 0)
+        printf("frames %d  magnified fps %.1f  (%.3f ms/frame, %d frames per call)\n", done,
+               timed / t_proc, 1e3 * t_proc / timed, B);
+    else
+        printf("frames %d\n", done);
+    if (fi) fclose(fi);
+    if (fo) fclose(fo);
+    free(host);
+    hipFree(d_in);
+    hipFree(d_out);
+    mm_destroy(h);
+    return 0;
+}

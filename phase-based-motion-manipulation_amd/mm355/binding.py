@@ -17,6 +17,8 @@ EDGE_CLAMP = 1
 MODE_PYRAMID = 0
 FRAMES_ON_DEVICE = 1
 
+KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv")   # MM_K_ROWS_FWD, MM_K_COLS, MM_K_ROWS_INV
+
 ERRORS = {0: "MM_OK", -1: "MM_ERR_INVALID", -2: "MM_ERR_UNSUPPORTED", -3: "MM_ERR_HIP",
           -4: "MM_ERR_NO_DEVICE", -5: "MM_ERR_OOM", -6: "MM_ERR_NO_STATE"}
 
@@ -80,6 +82,9 @@ def load_library(path=LIB_PATH):
         "mm_synth_frames": (ci, [vp, ci, ci, ci, ci, ctypes.c_uint64, ci, vp]),
         "mm_resample_table": (ci, [ci, ci, ci, ci, ctypes.POINTER(ctypes.c_int32),
                                    ctypes.POINTER(cf)]),
+        "mm_profile_begin": (ci, [vp]),
+        "mm_profile_end": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci),
+                                ctypes.POINTER(ci)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -192,6 +197,17 @@ class Handle:
     def compute_state(self, src, fmt, dev_buf, stream=None):
         check(lib().mm_compute_state(self.h, _ptr(src), fmt, _ptr(dev_buf), self.state_bytes,
                                      _ptr(stream)), "mm_compute_state")
+
+    def profile_begin(self):
+        check(lib().mm_profile_begin(self.h), "mm_profile_begin")
+
+    def profile_end(self):
+        """-> {kernel: (total_ms, launches, frames)} for K1/K2/K3."""
+        ms = (ctypes.c_double * 3)()
+        n = (ctypes.c_int * 3)()
+        f = (ctypes.c_int * 3)()
+        check(lib().mm_profile_end(self.h, ms, n, f), "mm_profile_end")
+        return {name: (ms[k], n[k], f[k]) for k, name in enumerate(KERNELS)}
 
     def synth(self, dev_out, t0, count, seed=0x5EED0000, gray=False, stream=None):
         check(lib().mm_synth_frames(_ptr(dev_out), self.width, self.height, t0, count, seed,
