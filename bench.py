@@ -36,9 +36,10 @@ def algorithmic_bytes(W, H, N, b_in=4, b_out=4):
     """B = W*H*(2*b_in + b_out) + 6*N^2*8 per output frame,
     split over the three kernels as they move it."""
     nn8 = N * N * 8
-    return {"k_rows_fwd": W * H * b_in + nn8,            # read frame, write row->col handoff
-            "k_cols": 4 * nn8,                          # handoff in/out + state in/out
-            "k_rows_inv": nn8 + W * H * (b_in + b_out),  # handoff in, frame in (I/Q), frame out
+    return {"k_rows_fwd": W * H * b_in + nn8,       # read frame, write row->col handoff
+            "k_cols": 4 * nn8,                     # handoff in/out + state in/out
+            "k_rows_inv": nn8,                     # col->row handoff in
+            "k_compose": W * H * (b_in + b_out),   # frame in (I/Q), frame out
             "frame": W * H * (2 * b_in + b_out) + 6 * nn8}
 
 

@@ -128,11 +128,13 @@ int mm_abi_version(void);
  * Kernel ids: */
 #define MM_K_ROWS_FWD 0   /* K1: resample + window + row real FFT      */
 #define MM_K_COLS     1   /* K2: column FFT + pyramid phase op + IFFT  */
-#define MM_K_ROWS_INV 2   /* K3: row C2R IFFT + blur + recombine + crop */
-#define MM_K_COUNT    3
+#define MM_K_ROWS_INV 2   /* K3: row C2R IFFT + |z| + horizontal blur    */
+#define MM_K_COMPOSE  3   /* K4: vertical blur + YIQ recombine + RGB + crop */
+#define MM_K_COUNT    4
 int mm_profile_begin(mm_handle *h);
 /* Waits for the recorded events; ms[k] = summed device ms, launches[k],
- * frames[k] = frames processed by kernel k (any pointer may be NULL). */
+ * frames[k] = frames processed by kernel k, k < MM_K_COUNT (arrays of
+ * MM_K_COUNT entries; any pointer may be NULL). */
 int mm_profile_end(mm_handle *h, double *ms, int *launches, int *frames);
 
 /* Synthetic stream frames generated on the device:

@@ -44,7 +44,8 @@ struct mm_handle {
     Tap4 *d_col, *d_row;
     c2 *d_tw;
     c2 *d_G, *d_Q, *d_state;
-    size_t g_stride, q_stride;  // elements per frame
+    float *d_Yh;
+    size_t g_stride, q_stride, yh_stride;  // elements per frame
     int chunk;                  // frames per K1/K2/K3 batch
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
@@ -135,8 +136,12 @@ static void build_spec(const mm_params &p, int N, Spec &sp)
     sp.minF = p.min_freq;
     sp.maxF = p.max_freq;
     sp.S = p.phase_scale;
-    sp.tau = p.magnitude_threshold;
+    sp.tau2 = p.magnitude_threshold * p.magnitude_threshold;
     sp.inv_nn = 1.0f / ((float)N * (float)N);
+    sp.hp_lo = p.max_freq * 0.8f;             // PyramidOperations.compute:36-41
+    sp.hp_inv = 1.0f / (p.max_freq * 0.2f);
+    sp.lp_hi = p.min_freq * 1.2f;             // PyramidOperations.compute:48-53
+    sp.lp_inv = 1.0f / (p.min_freq * 0.2f);
     for (int i = 1; i < p.levels - 1; ++i) {
         // PyramidOperations.compute:59-64 (L=3: 0/0 = NaN -> empty band)
         volatile float num = (float)(i - 1), den = (float)(p.levels - 3);
@@ -145,6 +150,7 @@ static void build_spec(const mm_params &p, int N, Spec &sp)
         const float bwid = center * 0.5f;
         sp.lo[i] = center - bwid;
         sp.hi[i] = center + bwid;
+        sp.inv_w[i] = 1.0f / (sp.hi[i] - sp.lo[i]);
     }
 }
 
@@ -179,30 +185,11 @@ template <int LOG2N> static size_t lds_fft_bytes()
 {
     return sizeof(c2) * (size_t)groups_per_wg<LOG2N>() * lds_complex<(1 << LOG2N)>();
 }
-template <int LOG2N> static size_t lds_k3_bytes(int W)
-{
-    return lds_fft_bytes<LOG2N>() + sizeof(float) * (size_t)k3_ring<LOG2N>() * W;
-}
-
 template <int LOG2N>
 static int set_attrs(int W)
 {
-    const size_t k3 = lds_k3_bytes<LOG2N>(W);
-    HIPCHK(hipFuncSetAttribute((const void *)k_rows_inv<LOG2N, 0>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3));
-    HIPCHK(hipFuncSetAttribute((const void *)k_rows_inv<LOG2N, 1>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3));
+    (void)W;   // every kernel stays within the default 64 KiB dynamic LDS
     return MM_OK;
-}
-
-static int k3_band_rows(const mm_handle *h, int nframes)
-{
-    // enough work-groups to fill 256 CUs, bands >= 8 rows to bound the 4-row halo
-    const int target = 1024;
-    int br = (int)(((long long)h->H * nframes + target - 1) / target);
-    br = std::max(br, 8);
-    br = (br + 1) & ~1;
-    return std::min(br, h->H);
 }
 
 template <int LOG2N>
@@ -247,19 +234,28 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
 {
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
-    const int br = k3_band_rows(h, nout);
-    const int bands = (h->H + br - 1) / br;
+    const int ppf = h->geo.Hn / 2;
+    const int total = ppf * nout;
+    const int gpw = groups_per_wg<LOG2N>();
+    {
+        ProfScope ps(h, s, MM_K_ROWS_INV, nout);
+        hipLaunchKernelGGL((k_rows_inv<LOG2N>), dim3((total + gpw - 1) / gpw),
+                           dim3(wg_threads<LOG2N>()), lds_fft_bytes<LOG2N>(), s, h->d_Q,
+                           h->q_stride, h->d_Yh, h->yh_stride, frame0, ppf, total, h->geo,
+                           h->blur, h->d_tw);
+        HIPCHK(hipGetLastError());
+    }
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-    const size_t lds = lds_k3_bytes<LOG2N>(h->W);
-    ProfScope ps(h, s, MM_K_ROWS_INV, nout);
+    const size_t lds = sizeof(float) * 2 * h->W;
+    ProfScope ps(h, s, MM_K_COMPOSE, nout);
     if (fmt == MM_RGBA8)
-        hipLaunchKernelGGL((k_rows_inv<LOG2N, 0>), dim3(bands * nout), dim3(wg_threads<LOG2N>()),
-                           lds, s, h->d_Q, h->q_stride, in, out, fb, frame0, bands, br, h->geo,
-                           h->blur, h->d_col, h->d_row, h->d_tw);
+        hipLaunchKernelGGL((k_compose<0>), dim3(h->H * nout), dim3(kComposeThreads), lds, s,
+                           h->d_Yh, h->yh_stride, in, out, fb, frame0, h->geo, h->blur, h->d_col,
+                           h->d_row);
     else
-        hipLaunchKernelGGL((k_rows_inv<LOG2N, 1>), dim3(bands * nout), dim3(wg_threads<LOG2N>()),
-                           lds, s, h->d_Q, h->q_stride, in, out, fb, frame0, bands, br, h->geo,
-                           h->blur, h->d_col, h->d_row, h->d_tw);
+        hipLaunchKernelGGL((k_compose<1>), dim3(h->H * nout), dim3(kComposeThreads), lds, s,
+                           h->d_Yh, h->yh_stride, in, out, fb, frame0, h->geo, h->blur, h->d_col,
+                           h->d_row);
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -407,6 +403,7 @@ static void free_handle(mm_handle *h)
     (void)hipFree(h->d_tw);
     (void)hipFree(h->d_G);
     (void)hipFree(h->d_Q);
+    (void)hipFree(h->d_Yh);
     (void)hipFree(h->d_state);
     (void)hipFree(h->d_stage_in);
     (void)hipFree(h->d_stage_out);
@@ -472,6 +469,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->chunk = ch ? std::max(1, atoi(ch)) : (N >= 4096 ? 4 : 8);
     h->g_stride = (size_t)(N / 2 + 1) * height;
     h->q_stride = (size_t)(N / 2 + 1) * g.Hq;
+    h->yh_stride = (size_t)g.Hn * width;
 
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         free_handle(h);
@@ -482,6 +480,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
               hipMalloc(&h->d_tw, sizeof(c2) * N) == hipSuccess &&
               hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * h->chunk) == hipSuccess &&
               hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * h->chunk) == hipSuccess &&
+              hipMalloc(&h->d_Yh, sizeof(float) * h->yh_stride * h->chunk) == hipSuccess &&
               hipMalloc(&h->d_state, sizeof(c2) * (size_t)(N / 2 + 1) * N) == hipSuccess;
     if (!ok) {
         free_handle(h);
@@ -640,8 +639,8 @@ int mm_profile_begin(mm_handle *h)
 int mm_profile_end(mm_handle *h, double *ms, int *launches, int *frames)
 {
     if (!h) return MM_ERR_INVALID;
-    double t[MM_K_COUNT] = {0, 0, 0};
-    int n[MM_K_COUNT] = {0, 0, 0}, f[MM_K_COUNT] = {0, 0, 0};
+    double t[MM_K_COUNT] = {};
+    int n[MM_K_COUNT] = {}, f[MM_K_COUNT] = {};
     int rc = MM_OK;
     for (auto &r : h->prof_recs) {
         float e = 0.0f;

@@ -97,8 +97,21 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *_
 #pragma unroll
         for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
         if (NS > 1) {
+            // one table load per butterfly; W^m by products (<= 3 roundings)
+            c2 w[R];
+            w[1] = twiddle<DIR>(tw, k * TWS);
+            if (R >= 4) {
+                w[2] = mul(w[1], w[1]);
+                w[3] = mul(w[2], w[1]);
+            }
+            if (R == 8) {
+                w[4] = mul(w[2], w[2]);
+                w[5] = mul(w[4], w[1]);
+                w[6] = mul(w[4], w[2]);
+                w[7] = mul(w[4], w[3]);
+            }
 #pragma unroll
-            for (int m = 1; m < R; ++m) u[m] = mul(u[m], twiddle<DIR>(tw, m * k * TWS));
+            for (int m = 1; m < R; ++m) u[m] = mul(u[m], w[m]);
         }
         if (R == 8) dft8<DIR>(u);
         else if (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);

@@ -7,9 +7,9 @@
 //                   A --IFFT--> Q[f][row]; F_t becomes the state.  One WG owns
 //                   a column for a whole chunk of frames, so F_{t-1} stays in
 //                   registers between frames.
-//   K3 k_rows_inv : Q rows --(paired C2R IFFT)--> |z| --(5-tap H blur)--> ring
-//                   of rows in LDS --(5-tap V blur, YIQ recombine, YIQ->RGB,
-//                   saturate, crop)--> RGBA frame
+//   K3 k_rows_inv : Q rows --(paired C2R IFFT)--> |z| --(5-tap H blur)--> Yh
+//   K4 k_compose  : Yh --(5-tap V blur)--, input --(I/Q resample)--> YIQ->RGB,
+//                   saturate, crop --> RGBA frame
 // Reference stages replaced (MotionMagnificationProcessor.cs:145-206): a4-a18 of
 // SURVEY.md §8(a).  The pyramid levels are applied pointwise in frequency
 // (SURVEY.md §7): arg(m_i F) = arg F for real m_i >= 0, so one atan2/sincos per
@@ -39,8 +39,10 @@ struct Geo {
 
 struct Spec {
     int L;
-    float minF, maxF, S, tau, inv_nn;
-    float lo[kMaxLevels], hi[kMaxLevels];
+    float minF, maxF, S, tau2, inv_nn;
+    float hp_lo, hp_inv;    // high-pass ramp start maxF*0.8, 1/(maxF*0.2)
+    float lp_hi, lp_inv;    // low-pass ramp end minF*1.2, 1/(minF*0.2)
+    float lo[kMaxLevels], hi[kMaxLevels], inv_w[kMaxLevels];  // middle bands
 };
 
 struct Blur5 { float w0, w1, w2; };  // taps at 0, +-1, +-2 texels
@@ -181,52 +183,64 @@ __device__ __forceinline__ float smooth01(float x)   // HLSL smoothstep(0,1,x)
     return t * t * (3.0f - 2.0f * t);
 }
 
+// atan2 for the phase difference: octant reduction + degree-15 odd minimax
+// polynomial on [0,1] (|err| <= 1.5e-7 rad; the phase scale S multiplies it).
+__device__ __forceinline__ float fast_atan2(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float s = a * a;
+    float r = -0.00405455008149147f;
+    r = r * s + 0.021862903609871864f;
+    r = r * s - 0.055912263691425323f;
+    r = r * s + 0.09642193466424942f;
+    r = r * s - 0.1390862911939621f;
+    r = r * s + 0.19946566224098206f;
+    r = r * s - 0.33329859375953674f;
+    r = r * s + 0.9999993443489075f;
+    r *= a;
+    if (ay > ax) r = 1.57079632679489662f - r;
+    if (x < 0.0f) r = 3.14159265358979324f - r;
+    return copysignf(r, y);
+}
+
 // Radial masks of GeneratePyramidFilters (PyramidOperations.compute:25-87) and the
 // per-level gate/phase rule of ProcessPyramidPhaseDifference
 // (PyramidPhaseDifference.compute:58-101), summed over levels
-// (AccumulatePyramidLevel, PyramidOperations.compute:111-128), for one bin.
+// (AccumulatePyramidLevel, PyramidOperations.compute:111-128), for one bin:
+//   A = c * [ sum_{pass} m_i + sum_{mag} m_i * e^{i S wrap(arg p - arg c)} ] / N^2
+// Levels 0 and L-1 always pass; a middle level passes where |m c| or |m p| < tau.
 template <int LOG2N>
 __device__ __forceinline__ c2 pyramid_op(c2 c, c2 p, int fx, int fy, const Spec &sp)
 {
     constexpr int N = 1 << LOG2N;
-    const float ux = (float)fx / (float)N;
-    const float uy = (float)(fy <= N / 2 ? fy : N - fy) / (float)N;
-    const float fr = sqrtf(ux * ux + uy * uy);
-    const float cm = sqrtf(c.x * c.x + c.y * c.y);
-    const float pm = sqrtf(p.x * p.x + p.y * p.y);
-    const float mn = fminf(cm, pm);
-    float mpass = 0.0f, mmag = 0.0f;
-    for (int i = 0; i < sp.L; ++i) {
-        float m = 0.0f;
-        if (i == 0) {
-            if (fr > sp.maxF) m = 1.0f;
-            else if (fr > sp.maxF * 0.8f) m = smooth01((fr - sp.maxF * 0.8f) / (sp.maxF * 0.2f));
-        } else if (i == sp.L - 1) {
-            if (fr < sp.minF) m = 1.0f;
-            else if (fr < sp.minF * 1.2f) m = 1.0f - smooth01((fr - sp.minF) / (sp.minF * 0.2f));
-        } else {
-            const float lo = sp.lo[i], hi = sp.hi[i];
-            if (fr >= lo && fr <= hi) {
-                const float nrm = (fr - lo) / (hi - lo);
-                m = 0.5f * (1.0f + cosf(2.0f * kPi * (nrm - 0.5f)));
-            }
-        }
-        if (m > 0.0f) {
-            if (i == 0 || i == sp.L - 1 || m * mn < sp.tau) mpass += m;
+    const float ux = (float)fx * (1.0f / (float)N);
+    const float uy = (float)(fy <= N / 2 ? fy : N - fy) * (1.0f / (float)N);
+    const float fr = __builtin_amdgcn_sqrtf(ux * ux + uy * uy);
+    const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
+    // level 0: high-pass
+    float mpass = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
+    // level L-1: low-pass
+    if (sp.L > 1)
+        mpass += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+    float mmag = 0.0f;
+    for (int i = 1; i < sp.L - 1; ++i) {
+        if (fr >= sp.lo[i] && fr <= sp.hi[i]) {
+            const float m = 0.5f * (1.0f + __cosf(2.0f * kPi * ((fr - sp.lo[i]) * sp.inv_w[i] - 0.5f)));
+            if (m * m * mn2 < sp.tau2) mpass += m;
             else mmag += m;
         }
     }
-    c2 a = scale(c, mpass);
+    c2 a = scale(c, mpass * sp.inv_nn);
     if (mmag > 0.0f) {
         // delta = wrap(arg p - arg c) = arg(p * conj c)
-        const float dre = p.x * c.x + p.y * c.y;
-        const float dim = p.y * c.x - p.x * c.y;
-        const float d = atan2f(dim, dre);
-        float s, co;
-        sincosf(sp.S * d, &s, &co);
-        a = add(a, scale(mul(c, mk(co, s)), mmag));
+        const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
+        const float ph = sp.S * d;
+        const float k = mmag * sp.inv_nn;
+        a = add(a, scale(mul(c, mk(__cosf(ph), __sinf(ph))), k));
     }
-    return scale(a, sp.inv_nn);
+    return a;
 }
 
 template <int LOG2N>
@@ -237,7 +251,7 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = threadIdx.x / T, t = threadIdx.x % T;
+    const int grp = threadIdx.x / T, t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     const int f_raw = blockIdx.x * GPW + grp;
     const bool valid = f_raw <= N / 2;
@@ -246,9 +260,14 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
     c2 prev[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-        prev[j] = state_in ? state_in[(size_t)f * N + t + j * T] : mk(0.0f, 0.0f);
+        prev[j] = state_in ? state_in[(size_t)f * N + t0 + j * T] : mk(0.0f, 0.0f);
 
     for (int fr = 0; fr < nframes; ++fr) {
+        // Opaque per-iteration copy of the lane index: stops LICM from hoisting
+        // every t-derived LDS address and twiddle of both FFTs out of the frame
+        // loop (that pinned ~200 VGPRs and capped occupancy at 1 wave/SIMD).
+        int t = t0;
+        asm volatile("" : "+v"(t));
         const c2 *Gc = G + (size_t)fr * g_stride + (size_t)f * g.H;
         c2 v[8];
 #pragma unroll
@@ -264,10 +283,13 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+            // one bin at a time: keeps the 8 op instances from being interleaved
+            __builtin_amdgcn_sched_barrier(0);
             const c2 a = pyramid_op<LOG2N>(v[j], prev[j], f, t + j * T, sp);
             prev[j] = v[j];
             v[j] = a;
         }
+        __builtin_amdgcn_sched_barrier(0);
         fft_regs<LOG2N, +1>(v, t, lds, tw);
         if (valid) {
             c2 *Qc = Q + (size_t)fr * q_stride + (size_t)f * g.Hq;
@@ -280,131 +302,130 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
     }
     if (valid && state_out) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t + j * T] = prev[j];
+        for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t0 + j * T] = prev[j];
     }
 }
 
 // =========================================================================
-// K3: row C2R IFFT -> |z| -> blur -> YIQ recombine -> RGB -> crop
+// K3a: row C2R IFFT -> |z| -> horizontal blur -> Yh rows (fp32, global)
 // =========================================================================
-template <int LOG2N> constexpr int k3_rows_per_step() { return 2 * groups_per_wg<LOG2N>(); }
-template <int LOG2N> constexpr int k3_ring() { return k3_rows_per_step<LOG2N>() + 4; }
-
-template <int LOG2N, int FMT>
+// One FFT group per pair of Q list rows (ka, ka+1); list row k is canvas row
+// (rb + k) mod N.  PerformIFFT (.cs:563-620) ends in |z| (FFT.compute:143-150);
+// the horizontal half of ApplyAntiAliasing (.cs:428-429) follows.
+template <int LOG2N>
 __global__ __launch_bounds__(wg_threads<LOG2N>())
-void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, const uint8_t *__restrict__ frames_in,
-                uint8_t *__restrict__ frames_out, size_t frame_bytes, int frame0,
-                int bands_per_frame, int BR, Geo g, Blur5 bw, const Tap4 *__restrict__ colTab,
-                const Tap4 *__restrict__ rowTab, const c2 *__restrict__ tw)
+void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Yh,
+                size_t yh_stride, int frame0, int pairs_per_frame, int total_pairs, Geo g,
+                Blur5 bw, const c2 *__restrict__ tw)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
-    constexpr int NT = wg_threads<LOG2N>();
-    constexpr int P = k3_rows_per_step<LOG2N>(), RING = k3_ring<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     const int grp = threadIdx.x / T, t = threadIdx.x % T;
-    c2 *scratch = lds_all;                                   // GPW FFT areas
-    c2 *lds = scratch + grp * lds_complex<N>();
-    float *ring = reinterpret_cast<float *>(scratch + GPW * lds_complex<N>());
-    float *scr_f = reinterpret_cast<float *>(scratch);
-
-    const int band = blockIdx.x % bands_per_frame;
-    const int frame = frame0 + blockIdx.x / bands_per_frame;
-    const int i0 = band * BR;
-    const int i1 = min(i0 + BR, g.H);
-    const int kend = i1 + 4;                       // list rows [i0, kend)
-    const c2 *Qf = Q + (size_t)frame * q_stride;
-    const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
-    uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
-
-    int next_emit = i0;
-    for (int s = i0; s < kend; s += P) {
-        // ---- paired C2R inverse row FFTs ---------------------------------
-        const int ka = s + 2 * grp, kb = ka + 1;
-        const bool ha = ka < kend, hb = kb < kend;
-        const int qa_row = ka % N, qb_row = kb % N;
-        c2 v[8];
+    c2 *lds = lds_all + grp * lds_complex<N>();
+    const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
+    const bool valid = logical < total_pairs;
+    const int frame = frame0 + (valid ? logical / pairs_per_frame : 0);
+    const int ka = valid ? 2 * (logical % pairs_per_frame) : 0;
+    const c2 *Qf = Q + (size_t)frame * q_stride + ka;
+    c2 v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int fq = t + j * T;
-            const bool mirror = fq > N / 2;
-            const int ff = mirror ? N - fq : fq;
-            c2 qa = ha ? Qf[(size_t)ff * g.Hq + qa_row] : mk(0.0f, 0.0f);
-            c2 qb = hb ? Qf[(size_t)ff * g.Hq + qb_row] : mk(0.0f, 0.0f);
-            if (ff == 0 || ff == N / 2) { qa.y = 0.0f; qb.y = 0.0f; }
-            if (mirror) { qa.y = -qa.y; qb.y = -qb.y; }
-            v[j] = mk(qa.x - qb.y, qa.y + qb.x);     // Z = Qa + i Qb
-        }
-        fft_regs<LOG2N, +1>(v, t, lds, tw);
-        // raw |z| rows of this group into its own scratch area
-        float *raw = reinterpret_cast<float *>(lds);
+    for (int j = 0; j < 8; ++j) {
+        const int fq = t + j * T;
+        const bool mirror = fq > N / 2;
+        const int ff = mirror ? N - fq : fq;
+        float4 q = valid ? *reinterpret_cast<const float4 *>(Qf + (size_t)ff * g.Hq)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ff == 0 || ff == N / 2) { q.y = 0.0f; q.w = 0.0f; }   // C2R: DC/Nyquist real
+        if (mirror) { q.y = -q.y; q.w = -q.w; }                   // X[N-f] = conj X[f]
+        v[j] = mk(q.x - q.w, q.y + q.z);                          // Z = Qa + i Qb
+    }
+    fft_regs<LOG2N, +1>(v, t, lds, tw);
+    float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows a, b
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            raw[t + j * T] = fabsf(v[j].x);
-            raw[N + t + j * T] = fabsf(v[j].y);
-        }
-        __syncthreads();
-        // ---- horizontal blur of the new rows into the ring ----------------
-        for (int e = threadIdx.x; e < P * g.W; e += NT) {
-            const int rl = e / g.W, X = e - rl * g.W;
-            const int k = s + rl;
-            if (k >= kend) continue;
-            const float *rw = reinterpret_cast<const float *>(scratch + (rl >> 1) * lds_complex<N>()) + (rl & 1) * N;
-            const int c = g.x0 + X;
-            float acc = bw.w0 * rw[wrap_idx(c, N, g.edge)];
+    for (int j = 0; j < 8; ++j) {
+        raw[t + j * T] = fabsf(v[j].x);
+        raw[N + t + j * T] = fabsf(v[j].y);
+    }
+    __syncthreads();
+    if (!valid) return;
+    float *out = Yh + (size_t)frame * yh_stride + (size_t)ka * g.W;
+    const bool interior = g.x0 >= 2 && g.x0 + g.W + 2 <= N;
+    for (int e = t; e < 2 * g.W; e += T) {
+        const int r = e >= g.W ? 1 : 0, X = e - r * g.W;
+        const float *rw = raw + r * N;
+        const int c = g.x0 + X;
+        float acc;
+        if (interior) {
+            acc = bw.w0 * rw[c] + bw.w1 * (rw[c - 1] + rw[c + 1]) + bw.w2 * (rw[c - 2] + rw[c + 2]);
+        } else {
+            acc = bw.w0 * rw[wrap_idx(c, N, g.edge)];
             acc += bw.w1 * (rw[wrap_idx(c - 1, N, g.edge)] + rw[wrap_idx(c + 1, N, g.edge)]);
             acc += bw.w2 * (rw[wrap_idx(c - 2, N, g.edge)] + rw[wrap_idx(c + 2, N, g.edge)]);
-            ring[(k % RING) * g.W + X] = acc;
         }
-        __syncthreads();
-        // ---- emit finished output rows -------------------------------------
-        const int avail = min(s + P, kend);        // list rows < avail are in the ring
-        while (next_emit < i1 && next_emit + 4 < avail) {
-            const int i = next_emit;
-            const Tap4 tr = rowTab[i];
-            float *VI = scr_f, *VQ = scr_f + g.W;
-            for (int x = threadIdx.x; x < g.W; x += NT) {
-                float vi = 0.0f, vq = 0.0f;
+        out[(size_t)r * g.W + X] = acc;
+    }
+}
+
+// =========================================================================
+// K3b: vertical blur -> YIQ recombine -> YIQ->RGB -> saturate -> crop
+// =========================================================================
+// One work-group per output row: the vertical half of ApplyAntiAliasing
+// (.cs:430-431), CombineYIQChannels (.cs:437-442; I/Q of the windowed, padded
+// current frame re-derived from the input through the same composite taps as
+// K1), the YIQ->RGB blit (.cs:200-204) and CropTexture (.cs:386-410).
+constexpr int kComposeThreads = 256;
+
+template <int FMT>
+__global__ __launch_bounds__(kComposeThreads)
+void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__restrict__ frames_in,
+               uint8_t *__restrict__ frames_out, size_t frame_bytes, int frame0, Geo g,
+               Blur5 bw, const Tap4 *__restrict__ colTab, const Tap4 *__restrict__ rowTab)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds_f[];
+    float *VI = lds_f, *VQ = lds_f + g.W;
+    const int i = blockIdx.x % g.H;                      // output (image) row
+    const int frame = frame0 + blockIdx.x / g.H;
+    const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
+    const Tap4 tr = rowTab[i];
+    for (int x = threadIdx.x; x < g.W; x += kComposeThreads) {
+        float vi = 0.0f, vq = 0.0f;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float4 px = Pix<FMT>::load(img, (size_t)tr.idx[m] * g.W + x);
-                    vi += tr.w[m] * chroma_i(px);
-                    vq += tr.w[m] * chroma_q(px);
-                }
-                VI[x] = vi;
-                VQ[x] = vq;
-            }
-            __syncthreads();
-            // canvas row Y = y0 + i; a blur tap at wrapped/clamped canvas row cy
-            // is the band's sequential list row in [i, i+4] congruent to cy - rb.
-            const int Y = g.y0 + i;
-            int sl[5];
-#pragma unroll
-            for (int d = 0; d < 5; ++d) {
-                const int cy = wrap_idx(Y + d - 2, N, g.edge);
-                const int kk = (cy - g.rb + 2 * N) & (N - 1);
-                const int kseq = i + ((kk - i + 2 * N) & (N - 1));
-                sl[d] = (kseq % RING) * g.W;
-            }
-            for (int X = threadIdx.x; X < g.W; X += NT) {
-                float yb = bw.w0 * ring[sl[2] + X];
-                yb += bw.w1 * (ring[sl[1] + X] + ring[sl[3] + X]);
-                yb += bw.w2 * (ring[sl[0] + X] + ring[sl[4] + X]);
-                const Tap4 tc = colTab[X];
-                float ci = 0.0f, cq = 0.0f;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    ci += tc.w[c] * VI[tc.idx[c]];
-                    cq += tc.w[c] * VQ[tc.idx[c]];
-                }
-                // YIQToRGB.shader:51-76 + saturate
-                const float r = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
-                const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
-                const float b = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
-                Pix<FMT>::store(outp, (size_t)i * g.W + X, r, gg, b);
-            }
-            __syncthreads();
-            ++next_emit;
+        for (int m = 0; m < 4; ++m) {
+            const float4 px = Pix<FMT>::load(img, (size_t)tr.idx[m] * g.W + x);
+            vi += tr.w[m] * chroma_i(px);
+            vq += tr.w[m] * chroma_q(px);
         }
+        VI[x] = vi;
+        VQ[x] = vq;
+    }
+    // Yh rows of the 5 vertical taps (canvas rows wrapped/clamped -> list rows)
+    const float *yr[5];
+    const int Y = g.y0 + i;
+    const float *Yf = Yh + (size_t)frame * yh_stride;
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+        const int cy = wrap_idx(Y + d - 2, g.N, g.edge);
+        const int k = (cy - g.rb + 2 * g.N) & (g.N - 1);
+        yr[d] = Yf + (size_t)k * g.W;
+    }
+    __syncthreads();
+    uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
+    for (int X = threadIdx.x; X < g.W; X += kComposeThreads) {
+        float yb = bw.w0 * yr[2][X];
+        yb += bw.w1 * (yr[1][X] + yr[3][X]);
+        yb += bw.w2 * (yr[0][X] + yr[4][X]);
+        const Tap4 tc = colTab[X];
+        float ci = 0.0f, cq = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            ci += tc.w[c] * VI[tc.idx[c]];
+            cq += tc.w[c] * VQ[tc.idx[c]];
+        }
+        // YIQToRGB.shader:51-76 + saturate
+        const float r = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
+        const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
+        const float b = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
+        Pix<FMT>::store(outp, (size_t)i * g.W + X, r, gg, b);
     }
 }
 

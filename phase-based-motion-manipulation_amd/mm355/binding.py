@@ -17,7 +17,7 @@ EDGE_CLAMP = 1
 MODE_PYRAMID = 0
 FRAMES_ON_DEVICE = 1
 
-KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv")   # MM_K_ROWS_FWD, MM_K_COLS, MM_K_ROWS_INV
+KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv", "k_compose")   # MM_K_* ids 0..3
 
 ERRORS = {0: "MM_OK", -1: "MM_ERR_INVALID", -2: "MM_ERR_UNSUPPORTED", -3: "MM_ERR_HIP",
           -4: "MM_ERR_NO_DEVICE", -5: "MM_ERR_OOM", -6: "MM_ERR_NO_STATE"}
@@ -202,10 +202,11 @@ class Handle:
         check(lib().mm_profile_begin(self.h), "mm_profile_begin")
 
     def profile_end(self):
-        """-> {kernel: (total_ms, launches, frames)} for K1/K2/K3."""
-        ms = (ctypes.c_double * 3)()
-        n = (ctypes.c_int * 3)()
-        f = (ctypes.c_int * 3)()
+        """-> {kernel: (total_ms, launches, frames)} for every kernel of the path."""
+        k = len(KERNELS)
+        ms = (ctypes.c_double * k)()
+        n = (ctypes.c_int * k)()
+        f = (ctypes.c_int * k)()
         check(lib().mm_profile_end(self.h, ms, n, f), "mm_profile_end")
         return {name: (ms[k], n[k], f[k]) for k, name in enumerate(KERNELS)}
 
