@@ -170,3 +170,29 @@ def test_c3_2160p_vs_oracle():
     gf = T.gpu_run(W, H, ff, 6, 25.0)
     assert np.array_equal(gf[0], ff[0])
     T.assert_close_f32(gf[1], rf[1])
+
+
+def test_chunk_boundary_state_handoff():
+    """What the multi-GPU ring carries: rank g's state = mm_compute_state of the
+    frame before its chunk.  Two handles ("ranks") reproduce one stream bitwise."""
+    import torch
+    import mm355
+    W, H, C = 200, 120, 5
+    fr = T.synth(W, H, 2 * C, fmt="u8")
+    full = T.gpu_run(W, H, fr, 5, 25.0, mode="stream")
+    p = mm355.Params.make(phase_scale=25.0)
+    r0, r1 = mm355.Handle(W, H, p), mm355.Handle(W, H, p)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    out = torch.empty_like(dev)
+    st = torch.empty(r1.state_bytes, dtype=torch.uint8, device="cuda")
+    r0.compute_state(dev[C - 1], mm355.RGBA8, st)          # rank 0's last frame
+    torch.cuda.synchronize()
+    r1.set_state(st)
+    r0.process_stream(dev[:C], out[:C], C, mm355.RGBA8)
+    r1.process_stream(dev[C:], out[C:], C, mm355.RGBA8)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for k in range(2 * C):
+        assert np.array_equal(got[k], full[k]), k
+    r0.close()
+    r1.close()
