@@ -218,11 +218,12 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
                      c2 *st_out, hipStream_t s)
 {
     const int gpw = groups_per_wg<LOG2N>();
-    const int cols = (1 << LOG2N) / 2 + 1;
+    const int cols = (1 << LOG2N) / 2;   // f = 0 and f = N/2 share group 0 (k_cols)
     const int blocks = (cols + gpw - 1) / gpw;
     ProfScope ps(h, s, MM_K_COLS, nframes);
+    // two LDS areas per group: FFT exchange + the packed (0, N/2) column pair's A
     hipLaunchKernelGGL((k_cols<LOG2N>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                       lds_fft_bytes<LOG2N>(), s, h->d_G, h->g_stride, h->d_Q, h->q_stride,
+                       2 * lds_fft_bytes<LOG2N>(), s, h->d_G, h->g_stride, h->d_Q, h->q_stride,
                        st_in, st_out, nframes, first_passthrough, h->geo, h->spec, h->d_tw);
     HIPCHK(hipGetLastError());
     return MM_OK;

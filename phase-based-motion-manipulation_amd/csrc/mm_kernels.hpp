@@ -243,6 +243,13 @@ __device__ __forceinline__ c2 pyramid_op(c2 c, c2 p, int fx, int fy, const Spec 
     return a;
 }
 
+// Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
+// f = N/2 (row DFT bins that are real for real rows, so their column spectra are
+// Hermitian in fy) share group 0 of block 0 as one complex column z = G0 + i*GN:
+// the pyramid op runs on fy <= N/2 for both and the upper half is mirrored.  The
+// grid is then exactly N/2 groups (1024 at N=2048: one resident round at 4
+// WGs/CU instead of 1025 with a one-WG tail).  Column N/2's F_{t-1} lives in the
+// state buffer between frames.
 template <int LOG2N>
 __global__ __launch_bounds__(wg_threads<LOG2N>())
 void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_t q_stride,
@@ -254,8 +261,11 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
     const int grp = threadIdx.x / T, t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     const int f_raw = blockIdx.x * GPW + grp;
-    const bool valid = f_raw <= N / 2;
-    const int f = valid ? f_raw : N / 2;
+    const bool valid = f_raw < N / 2;
+    const int f = valid ? f_raw : N / 2 - 1;
+    const bool blk0 = blockIdx.x == 0;        // uniform: block 0 runs the extra exchanges
+    const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
+    c2 *stN = state_out + (size_t)(N / 2) * N;
 
     c2 prev[8];
 #pragma unroll
@@ -269,38 +279,100 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
         int t = t0;
         asm volatile("" : "+v"(t));
         const c2 *Gc = G + (size_t)fr * g_stride + (size_t)f * g.H;
+        const c2 *GN = G + (size_t)fr * g_stride + (size_t)(N / 2) * g.H;
         c2 v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int rr = t + j * T - g.y0;
-            v[j] = (rr >= 0 && rr < g.H) ? Gc[rr] : mk(0.0f, 0.0f);
+            const bool in = rr >= 0 && rr < g.H;
+            if (packed)     // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
+                v[j] = in ? mk(Gc[rr].x, GN[rr].x) : mk(0.0f, 0.0f);
+            else
+                v[j] = in ? Gc[rr] : mk(0.0f, 0.0f);
         }
         fft_regs<LOG2N, -1>(v, t, lds, tw);
-        if (fr == 0 && first_passthrough) {
+        const bool pass_frame = fr == 0 && first_passthrough;
+        if (blk0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) prev[j] = v[j];
+            for (int j = 0; j < 8; ++j) lds[pad8(t + j * T)] = v[j];
+            __syncthreads();
+        }
+        if (packed) {
+            // unpack Z = F0 + i FN:  F0 = (Z + conj Zm)/2, FN = (Z - conj Zm)/2i, Zm = Z[N-fy]
+            c2 *A0 = lds + lds_complex<N>(), *AN = A0 + (N / 2 + 1);
+            const c2 *pNsrc = fr ? stN : (state_in ? state_in + (size_t)(N / 2) * N : nullptr);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __builtin_amdgcn_sched_barrier(0);
+                const int fy = t + j * T;
+                const c2 z = lds[pad8(fy)], zm = lds[pad8((N - fy) & (N - 1))];
+                const c2 f0 = mk(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+                const c2 fN = mk(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+                if (!pass_frame && fy <= N / 2) {
+                    const c2 pn = pNsrc ? pNsrc[fy] : mk(0.0f, 0.0f);
+                    A0[fy] = pyramid_op<LOG2N>(f0, prev[j], 0, fy, sp);
+                    AN[fy] = pyramid_op<LOG2N>(fN, pn, N / 2, fy, sp);
+                }
+                prev[j] = f0;
+                stN[fy] = fN;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (pass_frame) {
+            if (!packed) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) prev[j] = v[j];
+            }
+            if (blk0) __syncthreads();
             continue;
         }
+        if (blk0) {
+            __syncthreads();
+            if (packed) {
+                const c2 *A0 = lds + lds_complex<N>(), *AN = A0 + (N / 2 + 1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            // one bin at a time: keeps the 8 op instances from being interleaved
-            __builtin_amdgcn_sched_barrier(0);
-            const c2 a = pyramid_op<LOG2N>(v[j], prev[j], f, t + j * T, sp);
-            prev[j] = v[j];
-            v[j] = a;
+                for (int j = 0; j < 8; ++j) {
+                    const int fy = t + j * T;
+                    const int src = fy <= N / 2 ? fy : N - fy;   // Hermitian: A[fy] = conj A[N-fy]
+                    c2 a0 = A0[src], an = AN[src];
+                    if (fy > N / 2) {
+                        a0.y = -a0.y;
+                        an.y = -an.y;
+                    }
+                    v[j] = mk(a0.x - an.y, a0.y + an.x);   // A0 + i AN
+                }
+            }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if (!packed) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // one bin at a time: keeps the 8 op instances from being interleaved
+                __builtin_amdgcn_sched_barrier(0);
+                const c2 a = pyramid_op<LOG2N>(v[j], prev[j], f, t + j * T, sp);
+                prev[j] = v[j];
+                v[j] = a;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
         fft_regs<LOG2N, +1>(v, t, lds, tw);
         if (valid) {
             c2 *Qc = Q + (size_t)fr * q_stride + (size_t)f * g.Hq;
+            c2 *QN = Q + (size_t)fr * q_stride + (size_t)(N / 2) * g.Hq;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-                if (k < g.Hn) Qc[k] = v[j];
+                if (k < g.Hn) {
+                    if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
+                        Qc[k] = mk(v[j].x, 0.0f);
+                        QN[k] = mk(v[j].y, 0.0f);
+                    } else {
+                        Qc[k] = v[j];
+                    }
+                }
             }
         }
     }
-    if (valid && state_out) {
+    if (valid) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t0 + j * T] = prev[j];
     }
@@ -383,8 +455,10 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
 {
     extern __shared__ __attribute__((aligned(16))) float lds_f[];
     float *VI = lds_f, *VQ = lds_f + g.W;
-    const int i = blockIdx.x % g.H;                      // output (image) row
-    const int frame = frame0 + blockIdx.x / g.H;
+    // consecutive rows (which share Yh rows and source rows) on one XCD's L2
+    const int row = xcd_remap(blockIdx.x, gridDim.x);
+    const int i = row % g.H;                             // output (image) row
+    const int frame = frame0 + row / g.H;
     const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
     const Tap4 tr = rowTab[i];
     for (int x = threadIdx.x; x < g.W; x += kComposeThreads) {

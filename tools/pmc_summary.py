@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs into profiles/traffic.json.
+
+FETCH_SIZE and WRITE_SIZE are in KiB (x1024 for bytes).  On gfx950 FETCH_SIZE
+under-reads wide streaming loads (MI355X_MICROARCH.md §HBM); each counter is
+corrected by the factor measured on tools/pmc_calib (512 MiB streamed at the
+access width that dominates the kernel's traffic).
+
+usage: pmc_summary.py FETCH_DIR WRITE_DIR CAL_FETCH_DIR CAL_WRITE_DIR FRAMES_PER_LAUNCH OUT
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+# dominant (read width, write width) in bytes per lane, per kernel
+WIDTHS = {"k_rows_fwd": (4, 16), "k_cols": (8, 8), "k_rows_inv": (16, 4), "k_compose": (4, 4)}
+CAL_BYTES = 512 << 20
+
+
+def short(name):
+    m = re.search(r"mm::(k_[a-z_]+)", name)
+    if m:
+        return m.group(1)
+    m = re.search(r"\b(rd|wr)<(float|HIP_vector_type<float, (\d)u>)", name)
+    if not m:
+        return None
+    return f"{m.group(1)}_{4 * int(m.group(3) or 1)}"
+
+
+def read_counter(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != counter:
+                continue
+            k = short(row.get("Kernel_Name", ""))
+            if k:
+                vals[k].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    fdir, wdir, cfdir, cwdir, fpl, out = sys.argv[1:7]
+    fpl = int(fpl)
+    fetch, write = read_counter(fdir, "FETCH_SIZE"), read_counter(wdir, "WRITE_SIZE")
+    cfetch, cwrite = read_counter(cfdir, "FETCH_SIZE"), read_counter(cwdir, "WRITE_SIZE")
+    fcorr = {w: CAL_BYTES / (cfetch[f"rd_{w}"] * 1024) for w in (4, 8, 16) if cfetch.get(f"rd_{w}")}
+    wcorr = {w: CAL_BYTES / (cwrite[f"wr_{w}"] * 1024) for w in (4, 8, 16) if cwrite.get(f"wr_{w}")}
+    kernels = {}
+    for k, (rw, ww) in WIDTHS.items():
+        if k not in fetch or k not in write:
+            continue
+        fb, wb = fetch[k] * 1024, write[k] * 1024
+        fc, wc = fb * fcorr.get(rw, 1.0), wb * wcorr.get(ww, 1.0)
+        kernels[k] = {"fetch_bytes_raw": fb, "write_bytes_raw": wb,
+                      "fetch_bytes": fc, "write_bytes": wc,
+                      "hbm_bytes_per_launch": fc + wc,
+                      "hbm_bytes_per_frame": (fc + wc) / fpl,
+                      "read_width": rw, "write_width": ww}
+    res = {"frames_per_launch": fpl, "calibration": {"fetch_factor": fcorr, "write_factor": wcorr},
+           "kernels": kernels,
+           "frame_hbm_bytes": sum(v["hbm_bytes_per_frame"] for v in kernels.values())}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
