@@ -32,15 +32,22 @@ METRIC = ("magnified frames/sec at 1920×1080, 5-level pyramid; "
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes(W, H, N, b_in=4, b_out=4):
-    """B = W*H*(2*b_in + b_out) + 6*N^2*8 per output frame,
-    split over the three kernels as they move it."""
-    nn8 = N * N * 8
-    return {"k_rows_fwd": W * H * b_in + nn8,       # read frame, write row->col handoff
-            "k_cols": 4 * nn8,                     # handoff in/out + state in/out
-            "k_rows_inv": nn8,                     # col->row handoff in
-            "k_compose": W * H * (b_in + b_out),   # frame in (I/Q), frame out
-            "frame": W * H * (2 * b_in + b_out) + 6 * nn8}
+def survey_bytes_per_frame(W, H, N, b_in=4, b_out=4):
+    """B = W*H*(2*b_in + b_out) + 6*N^2*8 per output frame
+    (dense N x N hand-offs, state read+write every frame)."""
+    return W * H * (2 * b_in + b_out) + 6 * N * N * 8
+
+
+def compulsory_bytes(W, H, N, frames, b_in=4, b_out=4):
+    """Per-launch algorithmic bytes of each kernel in this design: every input
+    and output byte it must move, once.  F = N/2+1 half-spectrum
+    columns, Hn = H+4 rows kept for the crop + vertical blur."""
+    F, Hn = N // 2 + 1, min(H + 4, N)
+    Hq = Hn + (Hn & 1)
+    return {"k_rows_fwd": frames * (W * H * b_in + F * H * 8),
+            "k_cols": frames * (F * H * 8 + F * Hq * 8) + 2 * F * N * 8,
+            "k_rows_inv": frames * (F * Hq * 8 + Hn * W * 4),
+            "k_compose": frames * (Hn * W * 4 + W * H * (b_in + b_out))}
 
 
 def parse():
@@ -175,25 +182,28 @@ def main():
 
     frames_total = a.steps * C * world
     fps = frames_total / elapsed
-    ab = algorithmic_bytes(W, H, N)
     kern = {}
     for name, (ms, launches, nfr) in prof.items():
         if launches:
+            ab = compulsory_bytes(W, H, N, nfr // launches)[name]
             kern[name] = {"ms_total": round(ms, 4), "launches": launches, "frames": nfr,
+                          "us_per_frame": round(ms * 1e3 / nfr, 3),
                           "ms_per_launch": round(ms / launches, 5),
-                          "algorithmic_bytes_per_launch": ab[name] * nfr / launches}
+                          "algorithmic_bytes_per_launch": ab,
+                          "achieved_GBps": round(ab / (ms / launches * 1e-3) / 1e9, 1)}
     dom = max(kern, key=lambda k: kern[k]["ms_total"])
     dk = kern[dom]
-    achieved = dk["algorithmic_bytes_per_launch"] / (dk["ms_per_launch"] * 1e-3) / 1e9
+    achieved = dk["achieved_GBps"]
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            if tj.get("frames_per_launch") == C and dom in tj.get("kernels", {}):
-                traffic = tj["kernels"][dom]["hbm_bytes_per_launch"]
+            per_frame = tj["kernels"][dom]["hbm_bytes_per_frame"]
+            traffic = round(per_frame * dk["frames"] / dk["launches"])
         except Exception:
             traffic = None
+    B = survey_bytes_per_frame(W, H, N)
 
     result = {
         "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
@@ -205,10 +215,16 @@ def main():
                    "frames_per_step_per_gpu": C, "padded_n": N,
                    "parallelism": (f"frame-sharded x{world}, RCCL ring state shift"
                                    if ring else f"replicas x{world}")},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                     "traffic": traffic},
-        "frame_algorithmic_GBps": round(ab["frame"] * fps / world / 1e9, 2),
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                     "bytes_model": "compulsory bytes of the dominant kernel (DESIGN.md §5); "
+                                    "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch"},
+        "survey_model": {"bytes_per_frame": B,
+                         "achieved_GBps_per_gpu": round(B * fps / world / 1e9, 1),
+                         "frac": round(B * fps / world / 1e9 / HBM_PEAK_GBPS, 4),
+                         "note": "SURVEY.md §8(d) B=W*H*(2b_in+b_out)+6*N^2*8; 100% = "
+                                 f"{HBM_PEAK_GBPS * 1e9 / B:.0f} frames/s per GPU"},
         "kernels": kern,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

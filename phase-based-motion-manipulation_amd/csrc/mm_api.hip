@@ -42,6 +42,7 @@ struct mm_handle {
     Spec spec;
     Blur5 blur;
     Tap4 *d_col, *d_row;
+    float4 *d_col3, *d_row3;    // the same taps merged onto offsets -1, 0, +1
     c2 *d_tw;
     c2 *d_G, *d_Q, *d_state;
     float *d_Yh;
@@ -117,14 +118,19 @@ static void build_tab(int S, int N, int edge, std::vector<Tap4> &tab)
             const int b = (int)bf;
             const float fr = ts - bf;
             const float wk = k ? gfr : 1.0f - gfr;
-            e.idx[2 * k] = wrap_host(b, S, edge);
+            // source indices stay UNWRAPPED (always in {i-1, i, i+1}); kernels wrap
+            // them with the edge mode on use (wrap_near)
+            e.idx[2 * k] = b;
             e.w[2 * k] = wk * (1.0f - fr);
-            e.idx[2 * k + 1] = wrap_host(b + 1, S, edge);
+            e.idx[2 * k + 1] = b + 1;
             e.w[2 * k + 1] = wk * fr;
         }
         const float wu = ((float)X + 0.5f) / (float)N;
         const float hann = 0.5f * (1.0f - cosf(2.0f * kPi * wu));
-        for (int m = 0; m < 4; ++m) e.w[m] *= hann;
+        for (int m = 0; m < 4; ++m) {
+            e.w[m] *= hann;
+            if (e.w[m] == 0.0f) e.idx[m] = i;   // zero taps (e.g. W == N) stay local
+        }
         tab[i] = e;
     }
 }
@@ -203,12 +209,12 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
     if (fmt == MM_RGBA8)
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col,
-                           h->d_row, h->d_tw, h->d_G, h->g_stride);
+                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+                           h->d_row3, h->d_tw, h->d_G, h->g_stride);
     else
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col,
-                           h->d_row, h->d_tw, h->d_G, h->g_stride);
+                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+                           h->d_row3, h->d_tw, h->d_G, h->g_stride);
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -247,16 +253,15 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
         HIPCHK(hipGetLastError());
     }
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-    const size_t lds = sizeof(float) * 2 * h->W;
+    const int rt = (h->H + kTileRows - 1) / kTileRows, ct = (h->W + kTileCols - 1) / kTileCols;
+    const dim3 grid(rt * ct * nout);
     ProfScope ps(h, s, MM_K_COMPOSE, nout);
     if (fmt == MM_RGBA8)
-        hipLaunchKernelGGL((k_compose<0>), dim3(h->H * nout), dim3(kComposeThreads), lds, s,
-                           h->d_Yh, h->yh_stride, in, out, fb, frame0, h->geo, h->blur, h->d_col,
-                           h->d_row);
+        hipLaunchKernelGGL((k_compose<0>), grid, dim3(kTileCols), 0, s, h->d_Yh, h->yh_stride,
+                           in, out, fb, frame0, rt, ct, h->geo, h->blur, h->d_col3, h->d_row3);
     else
-        hipLaunchKernelGGL((k_compose<1>), dim3(h->H * nout), dim3(kComposeThreads), lds, s,
-                           h->d_Yh, h->yh_stride, in, out, fb, frame0, h->geo, h->blur, h->d_col,
-                           h->d_row);
+        hipLaunchKernelGGL((k_compose<1>), grid, dim3(kTileCols), 0, s, h->d_Yh, h->yh_stride,
+                           in, out, fb, frame0, rt, ct, h->geo, h->blur, h->d_col3, h->d_row3);
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -390,7 +395,7 @@ int mm_resample_table(int width, int height, int axis, int edge_mode, int32_t *i
     build_tab(S, N, edge_mode, tab);
     for (int i = 0; i < S; ++i)
         for (int m = 0; m < 4; ++m) {
-            idx4[i * 4 + m] = tab[i].idx[m];
+            idx4[i * 4 + m] = wrap_host(tab[i].idx[m], S, edge_mode);
             w4[i * 4 + m] = tab[i].w[m];
         }
     return MM_OK;
@@ -401,6 +406,8 @@ static void free_handle(mm_handle *h)
     if (!h) return;
     (void)hipFree(h->d_col);
     (void)hipFree(h->d_row);
+    (void)hipFree(h->d_col3);
+    (void)hipFree(h->d_row3);
     (void)hipFree(h->d_tw);
     (void)hipFree(h->d_G);
     (void)hipFree(h->d_Q);
@@ -416,11 +423,34 @@ static void free_handle(mm_handle *h)
     delete h;
 }
 
+static bool taps_local(const std::vector<Tap4> &tab)
+{
+    for (size_t i = 0; i < tab.size(); ++i)
+        for (int m = 0; m < 4; ++m)
+            if (tab[i].idx[m] < (int)i - 1 || tab[i].idx[m] > (int)i + 1) return false;
+    return true;
+}
+
+static std::vector<float4> merge3(const std::vector<Tap4> &tab)
+{
+    std::vector<float4> out(tab.size());
+    for (size_t i = 0; i < tab.size(); ++i) {
+        float w[3] = {0.0f, 0.0f, 0.0f};
+        for (int m = 0; m < 4; ++m) w[tab[i].idx[m] - (int)i + 1] += tab[i].w[m];
+        out[i] = make_float4(w[0], w[1], w[2], 0.0f);
+    }
+    return out;
+}
+
 static int upload_tables(mm_handle *h)
 {
     std::vector<Tap4> col, row;
     build_tab(h->W, h->N, h->p.edge_mode, col);
     build_tab(h->H, h->N, h->p.edge_mode, row);
+    if (!taps_local(col) || !taps_local(row)) return MM_ERR_UNSUPPORTED;  // k_compose tiling
+    const std::vector<float4> c3 = merge3(col), r3 = merge3(row);
+    HIPCHK(hipMemcpy(h->d_col3, c3.data(), sizeof(float4) * h->W, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_row3, r3.data(), sizeof(float4) * h->H, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_col, col.data(), sizeof(Tap4) * h->W, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_row, row.data(), sizeof(Tap4) * h->H, hipMemcpyHostToDevice));
     return MM_OK;
@@ -478,6 +508,8 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     }
     bool ok = hipMalloc(&h->d_col, sizeof(Tap4) * width) == hipSuccess &&
               hipMalloc(&h->d_row, sizeof(Tap4) * height) == hipSuccess &&
+              hipMalloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
+              hipMalloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
               hipMalloc(&h->d_tw, sizeof(c2) * N) == hipSuccess &&
               hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * h->chunk) == hipSuccess &&
               hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * h->chunk) == hipSuccess &&
@@ -493,10 +525,13 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
         tw[k].x = (float)cos(a);
         tw[k].y = (float)sin(a);
     }
-    if (hipMemcpy(h->d_tw, tw.data(), sizeof(c2) * N, hipMemcpyHostToDevice) != hipSuccess ||
-        upload_tables(h) != MM_OK || do_set_attrs(h) != MM_OK) {
+    if (hipMemcpy(h->d_tw, tw.data(), sizeof(c2) * N, hipMemcpyHostToDevice) != hipSuccess) {
         free_handle(h);
         return MM_ERR_HIP;
+    }
+    if ((rc = upload_tables(h)) != MM_OK || (rc = do_set_attrs(h)) != MM_OK) {
+        free_handle(h);
+        return rc;
     }
     h->has_state = false;
     if (getenv("MM_DEBUG"))

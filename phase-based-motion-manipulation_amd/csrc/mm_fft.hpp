@@ -83,12 +83,20 @@ __device__ __forceinline__ c2 twiddle(const c2 *__restrict__ tw, int idx)
     return DIR < 0 ? w : mk(w.x, -w.y);
 }
 
+// Base twiddle W_{NS*R}^k of butterfly q of a pass (one table load).
+template <int N, int R, int NS, int DIR>
+__device__ __forceinline__ c2 pass_twiddle(int t, int q, const c2 *__restrict__ tw)
+{
+    constexpr int T = N / 8;
+    constexpr int TWS = N / (NS * R);  // twiddle-table stride for W_{NS*R}
+    return twiddle<DIR>(tw, ((t + q * T) & (NS - 1)) * TWS);
+}
+
 template <int N, int R, int NS, int DIR, bool LAST>
-__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
+__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *wb)
 {
     constexpr int T = N / 8;
     constexpr int B = 8 / R;
-    constexpr int TWS = N / (NS * R);  // twiddle-table stride for W_{NS*R}
 #pragma unroll
     for (int q = 0; q < B; ++q) {
         const int b = t + q * T;
@@ -97,9 +105,9 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *_
 #pragma unroll
         for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
         if (NS > 1) {
-            // one table load per butterfly; W^m by products (<= 3 roundings)
+            // base twiddle preloaded at FFT start; W^m by products (<= 3 roundings)
             c2 w[R];
-            w[1] = twiddle<DIR>(tw, k * TWS);
+            w[1] = wb[q];
             if (R >= 4) {
                 w[2] = mul(w[1], w[1]);
                 w[3] = mul(w[2], w[1]);
@@ -133,16 +141,34 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *_
     }
 }
 
-template <int LOG2N, int DIR, int P, int NS>
-__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
+template <int LOG2N> constexpr int fft_passes() { return LOG2N / 3 + (LOG2N % 3 ? 1 : 0); }
+template <int LOG2N, int P> constexpr int pass_radix()
 {
-    constexpr int R8 = LOG2N / 3;
-    constexpr int REM = LOG2N % 3;
-    constexpr int NP = R8 + (REM ? 1 : 0);
-    if constexpr (P < NP) {
-        constexpr int R = (P < R8) ? 8 : (REM == 2 ? 4 : 2);
-        fft_pass<(1 << LOG2N), R, NS, DIR, P == NP - 1>(v, t, lds, tw);
-        fft_pass_loop<LOG2N, DIR, P + 1, NS * R>(v, t, lds, tw);
+    return (P < LOG2N / 3) ? 8 : (LOG2N % 3 == 2 ? 4 : 2);
+}
+
+// Issue every pass's twiddle loads up front (slot P*4+q) so their latency hides
+// under the first pass instead of stalling each pass.
+template <int LOG2N, int DIR, int P, int NS>
+__device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
+{
+    if constexpr (P < fft_passes<LOG2N>()) {
+        constexpr int R = pass_radix<LOG2N, P>();
+        if constexpr (NS > 1) {
+#pragma unroll
+            for (int q = 0; q < 8 / R; ++q) wb[P * 4 + q] = pass_twiddle<(1 << LOG2N), R, NS, DIR>(t, q, tw);
+        }
+        preload_twiddles<LOG2N, DIR, P + 1, NS * R>(wb, t, tw);
+    }
+}
+
+template <int LOG2N, int DIR, int P, int NS>
+__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+{
+    if constexpr (P < fft_passes<LOG2N>()) {
+        constexpr int R = pass_radix<LOG2N, P>();
+        fft_pass<(1 << LOG2N), R, NS, DIR, P == fft_passes<LOG2N>() - 1>(v, t, lds, wb + P * 4);
+        fft_pass_loop<LOG2N, DIR, P + 1, NS * R>(v, t, lds, wb);
     }
 }
 
@@ -151,7 +177,9 @@ __device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const 
 template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
 {
-    fft_pass_loop<LOG2N, DIR, 0, 1>(v, t, lds, tw);
+    c2 wb[16];
+    preload_twiddles<LOG2N, DIR, 0, 1>(wb, t, tw);
+    fft_pass_loop<LOG2N, DIR, 0, 1>(v, t, lds, wb);
 }
 
 }  // namespace mm

@@ -58,6 +58,14 @@ __device__ __forceinline__ int wrap_idx(int i, int n, int edge)
     return r < 0 ? r + n : r;
 }
 
+// Wrap an index known to lie in [-1, n] (resample taps) with the edge mode.
+__device__ __forceinline__ int wrap_near(int i, int n, int edge)
+{
+    if (i < 0) return edge ? 0 : i + n;
+    if (i >= n) return edge ? n - 1 : i - n;
+    return i;
+}
+
 // Same-XCD blocks (b % 8 equal under round-robin dispatch) get consecutive ids.
 __device__ __forceinline__ int xcd_remap(int b, int nb)
 {
@@ -69,13 +77,18 @@ __device__ __forceinline__ int xcd_remap(int b, int nb)
 template <int FMT> struct Pix;
 template <> struct Pix<0> {           // RGBA8 UNORM
     static constexpr int bpp = 4;
-    __device__ static float4 load(const uint8_t *base, size_t i)
+    using raw_t = uint32_t;             // keep loads raw in registers, convert at use
+    __device__ static raw_t raw(const uint8_t *base, size_t i)
     {
-        uint32_t u = reinterpret_cast<const uint32_t *>(base)[i];
+        return reinterpret_cast<const uint32_t *>(base)[i];
+    }
+    __device__ static float4 cvt(raw_t u)
+    {
         const float s = 1.0f / 255.0f;
         return make_float4((float)(u & 255u) * s, (float)((u >> 8) & 255u) * s,
                            (float)((u >> 16) & 255u) * s, (float)(u >> 24) * s);
     }
+    __device__ static float4 load(const uint8_t *base, size_t i) { return cvt(raw(base, i)); }
     __device__ static void store(uint8_t *base, size_t i, float r, float g, float b)
     {
         uint32_t R = (uint32_t)(r * 255.0f + 0.5f), G = (uint32_t)(g * 255.0f + 0.5f),
@@ -85,10 +98,13 @@ template <> struct Pix<0> {           // RGBA8 UNORM
 };
 template <> struct Pix<1> {           // RGBA32F
     static constexpr int bpp = 16;
-    __device__ static float4 load(const uint8_t *base, size_t i)
+    using raw_t = float4;
+    __device__ static raw_t raw(const uint8_t *base, size_t i)
     {
         return reinterpret_cast<const float4 *>(base)[i];
     }
+    __device__ static float4 cvt(raw_t v) { return v; }
+    __device__ static float4 load(const uint8_t *base, size_t i) { return raw(base, i); }
     __device__ static void store(uint8_t *base, size_t i, float r, float g, float b)
     {
         reinterpret_cast<float4 *>(base)[i] = make_float4(r, g, b, 1.0f);
@@ -107,8 +123,8 @@ __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0
 template <int LOG2N, int FMT>
 __global__ __launch_bounds__(wg_threads<LOG2N>())
 void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pairs_per_frame,
-                int total_pairs, Geo g, const Tap4 *__restrict__ colTab,
-                const Tap4 *__restrict__ rowTab, const c2 *__restrict__ tw,
+                int total_pairs, Geo g, const float4 *__restrict__ colW3,
+                const float4 *__restrict__ rowW3, const c2 *__restrict__ tw,
                 c2 *__restrict__ G, size_t g_stride)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
@@ -121,36 +137,53 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     const int ra = valid ? 2 * (logical % pairs_per_frame) : 0;  // image row of pair
     const uint8_t *img = frames + (size_t)frame * frame_bytes;
 
-    // vertical part of the separable resample: V_a, V_b over all source columns
+    // vertical part of the separable resample: V_a, V_b over all source columns.
+    // Taps of image row r lie on source rows r-1..r+1 (w3 tables), so the pair
+    // (ra, ra+1) reads the 4 source rows ra-1..ra+2.
     float *V = reinterpret_cast<float *>(lds);
     if (valid) {
-        const Tap4 ta = rowTab[ra], tb = rowTab[ra + 1];
-        for (int i = t; i < g.W; i += T) {
-            float va = 0.0f, vb = 0.0f;
+        const float4 wa = rowW3[ra], wb = rowW3[ra + 1];
+        int sr[4];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                va += ta.w[m] * luma(Pix<FMT>::load(img, (size_t)ta.idx[m] * g.W + i));
-                vb += tb.w[m] * luma(Pix<FMT>::load(img, (size_t)tb.idx[m] * g.W + i));
+        for (int d = 0; d < 4; ++d) sr[d] = wrap_near(ra - 1 + d, g.H, g.edge);
+        // W <= N = 8T: at most 8 columns per thread, in two batches of 4 so the
+        // 16 loads of a batch are in flight together
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            __builtin_amdgcn_sched_barrier(0);
+            typename Pix<FMT>::raw_t px[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = min(t + (h * 4 + u) * T, g.W - 1);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) px[u][d] = Pix<FMT>::raw(img, (size_t)sr[d] * g.W + i);
             }
-            V[i] = va;
-            V[g.W + i] = vb;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = t + (h * 4 + u) * T;
+                float l[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) l[d] = luma(Pix<FMT>::cvt(px[u][d]));
+                if (i < g.W) {
+                    V[i] = wa.x * l[0] + wa.y * l[1] + wa.z * l[2];
+                    V[g.W + i] = wb.x * l[1] + wb.y * l[2] + wb.z * l[3];
+                }
+            }
         }
     }
     __syncthreads();
     c2 v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int i = t + j * T - g.x0;
-        float ya = 0.0f, yb = 0.0f;
-        if (valid && i >= 0 && i < g.W) {
-            const Tap4 tc = colTab[i];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                ya += tc.w[c] * V[tc.idx[c]];
-                yb += tc.w[c] * V[g.W + tc.idx[c]];
-            }
-        }
-        v[j] = mk(ya, yb);
+        if (j == 4) __builtin_amdgcn_sched_barrier(0);     // two batches: bound VGPRs
+        const int i = t + j * T - g.x0;                    // image column
+        const int ic = min(max(i, 0), g.W - 1);
+        const float4 w = colW3[ic];                         // source columns i-1, i, i+1
+        const int cl = wrap_near(ic - 1, g.W, g.edge), cr = wrap_near(ic + 1, g.W, g.edge);
+        const float ya = w.x * V[cl] + w.y * V[ic] + w.z * V[cr];
+        const float yb = w.x * V[g.W + cl] + w.y * V[g.W + ic] + w.z * V[g.W + cr];
+        const bool in = valid && i >= 0 && i < g.W;
+        v[j] = in ? mk(ya, yb) : mk(0.0f, 0.0f);
     }
     __syncthreads();
     fft_regs<LOG2N, -1>(v, t, lds, tw);
@@ -282,13 +315,14 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
         const c2 *GN = G + (size_t)fr * g_stride + (size_t)(N / 2) * g.H;
         c2 v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 8; ++j) {   // unconditional loads (clamped), then select
             const int rr = t + j * T - g.y0;
+            const int rc = min(max(rr, 0), g.H - 1);
+            const c2 a = Gc[rc];
+            const float bn = GN[rc].x;
             const bool in = rr >= 0 && rr < g.H;
-            if (packed)     // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
-                v[j] = in ? mk(Gc[rr].x, GN[rr].x) : mk(0.0f, 0.0f);
-            else
-                v[j] = in ? Gc[rr] : mk(0.0f, 0.0f);
+            // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
+            v[j] = in ? (packed ? mk(a.x, bn) : a) : mk(0.0f, 0.0f);
         }
         fft_regs<LOG2N, -1>(v, t, lds, tw);
         const bool pass_frame = fr == 0 && first_passthrough;
@@ -399,17 +433,23 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
     const int frame = frame0 + (valid ? logical / pairs_per_frame : 0);
     const int ka = valid ? 2 * (logical % pairs_per_frame) : 0;
     const c2 *Qf = Q + (size_t)frame * q_stride + ka;
+    float4 qv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // all 8 loads in flight (addresses always valid)
+        const int fq = t + j * T;
+        const int ff = fq > N / 2 ? N - fq : fq;
+        qv[j] = *reinterpret_cast<const float4 *>(Qf + (size_t)ff * g.Hq);
+    }
     c2 v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int fq = t + j * T;
         const bool mirror = fq > N / 2;
         const int ff = mirror ? N - fq : fq;
-        float4 q = valid ? *reinterpret_cast<const float4 *>(Qf + (size_t)ff * g.Hq)
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 q = qv[j];
         if (ff == 0 || ff == N / 2) { q.y = 0.0f; q.w = 0.0f; }   // C2R: DC/Nyquist real
         if (mirror) { q.y = -q.y; q.w = -q.w; }                   // X[N-f] = conj X[f]
-        v[j] = mk(q.x - q.w, q.y + q.z);                          // Z = Qa + i Qb
+        v[j] = valid ? mk(q.x - q.w, q.y + q.z) : mk(0.0f, 0.0f); // Z = Qa + i Qb
     }
     fft_regs<LOG2N, +1>(v, t, lds, tw);
     float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows a, b
@@ -439,67 +479,93 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
 }
 
 // =========================================================================
-// K3b: vertical blur -> YIQ recombine -> YIQ->RGB -> saturate -> crop
+// K4: vertical blur -> YIQ recombine -> YIQ->RGB -> saturate -> crop
 // =========================================================================
-// One work-group per output row: the vertical half of ApplyAntiAliasing
-// (.cs:430-431), CombineYIQChannels (.cs:437-442; I/Q of the windowed, padded
-// current frame re-derived from the input through the same composite taps as
-// K1), the YIQ->RGB blit (.cs:200-204) and CropTexture (.cs:386-410).
-constexpr int kComposeThreads = 256;
+// One work-group per tile of kTileRows output rows x kTileCols columns, one
+// column per thread: the vertical half of ApplyAntiAliasing (.cs:430-431) on
+// Yh, CombineYIQChannels (.cs:437-442; I/Q of the windowed, padded current frame
+// re-derived from the input through the same composite resample as K1), the
+// YIQ->RGB blit (.cs:200-204) and CropTexture (.cs:386-410).
+// The composite taps of image row/column i lie in {i-1, i, i+1} (checked on the
+// host), so they are merged into 3 weights (w3 tables) and a tile needs source
+// rows [i0-1, i0+TR] x columns [c0-1, c0+TC]: their I/Q are staged once in LDS;
+// the horizontal 3-tap combine of every staged row and the TR+4 Yh values of the
+// thread's column then live in registers.  One barrier per tile.
+constexpr int kTileRows = 8, kTileCols = 256;
 
 template <int FMT>
-__global__ __launch_bounds__(kComposeThreads)
+__global__ __launch_bounds__(kTileCols)
 void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__restrict__ frames_in,
-               uint8_t *__restrict__ frames_out, size_t frame_bytes, int frame0, Geo g,
-               Blur5 bw, const Tap4 *__restrict__ colTab, const Tap4 *__restrict__ rowTab)
+               uint8_t *__restrict__ frames_out, size_t frame_bytes, int frame0, int row_tiles,
+               int col_tiles, Geo g, Blur5 bw, const float4 *__restrict__ colW3,
+               const float4 *__restrict__ rowW3)
 {
-    extern __shared__ __attribute__((aligned(16))) float lds_f[];
-    float *VI = lds_f, *VQ = lds_f + g.W;
-    // consecutive rows (which share Yh rows and source rows) on one XCD's L2
-    const int row = xcd_remap(blockIdx.x, gridDim.x);
-    const int i = row % g.H;                             // output (image) row
-    const int frame = frame0 + row / g.H;
+    constexpr int TR = kTileRows, TC = kTileCols, WC = TC + 2;
+    __shared__ float2 iq[(TR + 2) * WC];     // I/Q of the staged source pixels
+    const int tid = threadIdx.x;
+    int b = blockIdx.x;
+    const int ct = b % col_tiles;
+    b /= col_tiles;
+    const int rt = b % row_tiles;
+    const int frame = frame0 + b / row_tiles;
+    const int i0 = rt * TR, c0 = ct * TC;
     const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
-    const Tap4 tr = rowTab[i];
-    for (int x = threadIdx.x; x < g.W; x += kComposeThreads) {
-        float vi = 0.0f, vq = 0.0f;
+
+    constexpr int E = (TR + 2) * WC, IT = (E + TC - 1) / TC;
+    typename Pix<FMT>::raw_t px[IT];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const float4 px = Pix<FMT>::load(img, (size_t)tr.idx[m] * g.W + x);
-            vi += tr.w[m] * chroma_i(px);
-            vq += tr.w[m] * chroma_q(px);
-        }
-        VI[x] = vi;
-        VQ[x] = vq;
+    for (int it = 0; it < IT; ++it) {   // all staging loads in flight, then convert
+        const int e = min(tid + it * TC, E - 1);
+        const int sr = e / WC, j = e - sr * WC;
+        const int row = wrap_near(min(i0 - 1 + sr, g.H), g.H, g.edge);
+        const int col = wrap_near(min(c0 - 1 + j, g.W), g.W, g.edge);
+        px[it] = Pix<FMT>::raw(img, (size_t)row * g.W + col);
     }
-    // Yh rows of the 5 vertical taps (canvas rows wrapped/clamped -> list rows)
-    const float *yr[5];
-    const int Y = g.y0 + i;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = tid + it * TC;
+        const float4 c = Pix<FMT>::cvt(px[it]);
+        if (e < E) iq[e] = make_float2(chroma_i(c), chroma_q(c));
+    }
+    const int X = c0 + tid;
+    const bool vx = X < g.W;
+    // Yh of this column for the TR+4 canvas rows y0+i0-2 .. y0+i0+TR+1 (wrapped
+    // or clamped like the blur's sampler, then mapped to Yh list rows)
     const float *Yf = Yh + (size_t)frame * yh_stride;
+    float yv[TR + 4];
 #pragma unroll
-    for (int d = 0; d < 5; ++d) {
-        const int cy = wrap_idx(Y + d - 2, g.N, g.edge);
+    for (int v = 0; v < TR + 4; ++v) {   // unconditional loads at clamped addresses
+        const int cy = wrap_near(g.y0 + i0 - 2 + v, g.N, g.edge);
         const int k = (cy - g.rb + 2 * g.N) & (g.N - 1);
-        yr[d] = Yf + (size_t)k * g.W;
+        const float y = Yf[(size_t)min(k, g.Hn - 1) * g.W + min(X, g.W - 1)];
+        yv[v] = k < g.Hn ? y : 0.0f;
     }
+    const float4 wc = vx ? colW3[X] : make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
-    uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
-    for (int X = threadIdx.x; X < g.W; X += kComposeThreads) {
-        float yb = bw.w0 * yr[2][X];
-        yb += bw.w1 * (yr[1][X] + yr[3][X]);
-        yb += bw.w2 * (yr[0][X] + yr[4][X]);
-        const Tap4 tc = colTab[X];
-        float ci = 0.0f, cq = 0.0f;
+    if (!vx) return;
+    float hi[TR + 2], hq[TR + 2];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            ci += tc.w[c] * VI[tc.idx[c]];
-            cq += tc.w[c] * VQ[tc.idx[c]];
+    for (int sr = 0; sr < TR + 2; ++sr) {
+        const float2 a = iq[sr * WC + tid], m = iq[sr * WC + tid + 1], c = iq[sr * WC + tid + 2];
+        hi[sr] = wc.x * a.x + wc.y * m.x + wc.z * c.x;
+        hq[sr] = wc.x * a.y + wc.y * m.y + wc.z * c.y;
+    }
+    uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
+#pragma unroll
+    for (int r = 0; r < TR; ++r) {
+        const int i = i0 + r;
+        if (i < g.H) {
+            const float4 wr = rowW3[i];                        // source rows i-1, i, i+1
+            const float ci = wr.x * hi[r] + wr.y * hi[r + 1] + wr.z * hi[r + 2];
+            const float cq = wr.x * hq[r] + wr.y * hq[r + 1] + wr.z * hq[r + 2];
+            const float yb = bw.w0 * yv[r + 2] + bw.w1 * (yv[r + 1] + yv[r + 3]) +
+                             bw.w2 * (yv[r] + yv[r + 4]);
+            // YIQToRGB.shader:51-76 + saturate
+            const float rr = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
+            const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
+            const float bb = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
+            Pix<FMT>::store(outp, (size_t)i * g.W + X, rr, gg, bb);
         }
-        // YIQToRGB.shader:51-76 + saturate
-        const float r = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
-        const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
-        const float b = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
-        Pix<FMT>::store(outp, (size_t)i * g.W + X, r, gg, b);
     }
 }
 
