@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--phase-scale", type=float, default=25.0)
     ap.add_argument("--mode", choices=("ring", "replicas"), default="ring")
+    ap.add_argument("--standard", action="store_true",
+                    help="usePyramidDecomposition=false (standard mode, SURVEY f1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="bound on the CPU-baseline sample")
@@ -143,7 +145,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     W, H, C = a.width, a.height, a.frames_per_step
     os.environ.setdefault("MM_CHUNK", str(C))
-    params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale)
+    params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
+                               mode=mm355.MODE_STANDARD if a.standard else mm355.MODE_PYRAMID)
     h = mm355.Handle(W, H, params, device=local)
     N = h.N
 
@@ -210,8 +213,10 @@ def main():
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
-                               f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)",
+        "config": {"workload": (f"{W}x{H} RGBA8 synthetic stream, standard (non-pyramid) mode, "
+                                f"PhaseScale={a.phase_scale}" if a.standard else
+                                f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
+                                f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)"),
                    "frames_per_step_per_gpu": C, "padded_n": N,
                    "parallelism": (f"frame-sharded x{world}, RCCL ring state shift"
                                    if ring else f"replicas x{world}")},

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 1
+#define MM_ABI_VERSION 2
 
 /* error codes */
 #define MM_OK               0
@@ -48,6 +48,7 @@ extern "C" {
 
 /* mm_params.mode */
 #define MM_MODE_PYRAMID   0   /* usePyramidDecomposition = true (.cs:18, :128-131) */
+#define MM_MODE_STANDARD  1   /* usePyramidDecomposition = false (.cs:132-135, :208-232) */
 /* mm_params.edge_mode: sampler wrap of the engine resamples and the blur
  * (unpinned by the reference) */
 #define MM_EDGE_REPEAT 0
@@ -58,7 +59,7 @@ extern "C" {
 
 typedef struct mm_handle mm_handle;
 
-/* Inspector fields of the reference component (.cs:12-31). */
+/* Inspector fields of the reference component (.cs:12-43). */
 typedef struct {
     int   levels;              /* pyramidLevels            .cs:19  (1..16)      */
     float min_freq;            /* minFrequency             .cs:20               */
@@ -66,12 +67,22 @@ typedef struct {
     float phase_scale;         /* phaseScale (PhaseScale)  .cs:29               */
     float magnitude_threshold; /* magnitudeThreshold=0.01  .cs:30               */
     int   orientations;        /* extension; must be 1 (reference semantics)    */
-    int   mode;                /* MM_MODE_PYRAMID                               */
+    int   mode;                /* MM_MODE_PYRAMID | MM_MODE_STANDARD            */
     int   edge_mode;           /* MM_EDGE_REPEAT | MM_EDGE_CLAMP                */
     int   apply_magnification; /* applyMotionMagnification .cs:12 (0: passthrough) */
+    /* standard mode's phase-delta band-pass (PhaseDifferenceComputeShader.compute:88-122) */
+    int   apply_bandpass_filter;  /* applyBandpassFilter  .cs:35 */
+    float low_frequency_cutoff;   /* lowFrequencyCutoff   .cs:36 */
+    float high_frequency_cutoff;  /* highFrequencyCutoff  .cs:37 */
+    float filter_steepness;       /* filterSteepness      .cs:38 */
+    float motion_sensitivity;     /* motionSensitivity    .cs:41 */
+    int   enhance_edges;          /* enhanceEdges         .cs:42 */
+    float edge_enhancement;       /* edgeEnhancement      .cs:43 (used iff enhance_edges, .cs:504) */
 } mm_params;
 
-/* Reference defaults: levels 5, 0.05/0.45, phaseScale 10, threshold 0.01. */
+/* Reference defaults (.cs:12-43): levels 5, 0.05/0.45, phaseScale 10, threshold
+ * 0.01, pyramid mode; band-pass on, 0.05/0.4, steepness 3, sensitivity 1.5,
+ * edges on at 0.8. */
 int mm_params_default(mm_params *p);
 
 /* Start()/InitializeProcessor (.cs:90-94, :289-342): geometry frozen here. */

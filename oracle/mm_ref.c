@@ -44,6 +44,9 @@ struct mm_ref {
     float *masks;            /* pyramidFilters, levels*N*N, .cs:680 */
     int masks_levels;
     float mask_min, mask_max;
+    /* standard (non-pyramid) mode, .cs:33-43 */
+    int standard, bp_apply;
+    float bp_low, bp_high, bp_steep, bp_sens, bp_edge;
 };
 
 /* ------------------------------------------------------------------ */
@@ -296,6 +299,47 @@ void mm_ref_mask(int n, int levels, int index, float min_freq, float max_freq,
         }
 }
 
+/* PhaseDifferenceComputeShader.compute:74-85 */
+static float spatial_frequency(int x, int y, int n)
+{
+    float fx = ((float)x / (float)n) - 0.5f;
+    float fy = ((float)y / (float)n) - 0.5f;
+    float freq = sqrtf(fx * fx + fy * fy);
+    float r = freq / 0.707f;
+    return r < 1.0f ? r : 1.0f;
+}
+
+/* PhaseDifferenceComputeShader.compute:88-122 */
+static float bandpass_weight(float sf, int apply, float low, float high, float steep,
+                             float sens, float edge)
+{
+    if (apply == 0) return 1.0f;
+    float weight = 1.0f;
+    if (sf < low) {
+        float ratio = sf / fmaxf(low, 0.001f);
+        weight *= powf(ratio, steep);
+    }
+    if (sf > high) {
+        float ratio = (1.0f - sf) / fmaxf(1.0f - high, 0.001f);
+        weight *= powf(ratio, steep);
+    }
+    weight *= sens;
+    if (sf > low && sf < high) {
+        float edge_factor = 1.0f + edge * sinf(PI_F * (sf - low) / (high - low));
+        weight *= edge_factor;
+    }
+    return fmaxf(weight, 0.0f);
+}
+
+void mm_ref_bandpass_weights(int n, int apply, float low, float high, float steep,
+                             float sens, float edge, float *out)
+{
+    for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x)
+            out[(size_t)y * n + x] =
+                bandpass_weight(spatial_frequency(x, y, n), apply, low, high, steep, sens, edge);
+}
+
 /* PyramidPhaseDifference.compute:47-54 */
 float mm_ref_normalize_phase(float phase)
 {
@@ -412,6 +456,7 @@ mm_ref *mm_ref_create(int width, int height, int levels, float min_freq,
     c->N = next_pow2(width > height ? width : height);  /* .cs:298-302 */
     c->apply = 1;
     c->first = 1;
+    mm_ref_set_standard(c, 0, 1, 0.05f, 0.4f, 3.0f, 1.5f, 0.8f);   /* .cs:35-43 */
     c->prev = (float *)calloc((size_t)width * height * 4, sizeof(float));
     mm_ref_set_params(c, levels, min_freq, max_freq, phase_scale, mag_threshold,
                       edge_mode);
@@ -443,6 +488,18 @@ void mm_ref_set_params(mm_ref *c, int levels, float min_freq, float max_freq,
 }
 
 void mm_ref_set_apply(mm_ref *c, int apply) { c->apply = apply; }
+
+void mm_ref_set_standard(mm_ref *c, int use_standard, int apply_bandpass, float low,
+                         float high, float steep, float sens, float edge)
+{
+    c->standard = use_standard;
+    c->bp_apply = apply_bandpass;
+    c->bp_low = low;
+    c->bp_high = high;
+    c->bp_steep = steep;
+    c->bp_sens = sens;
+    c->bp_edge = edge;
+}
 void mm_ref_reset(mm_ref *c) { c->first = 1; }
 
 size_t mm_ref_state_size(const mm_ref *c)
@@ -465,7 +522,8 @@ void mm_ref_set_state(mm_ref *c, const void *buf)
     memcpy(c->prev, (const char *)buf + 16, sizeof(float) * (size_t)c->W * c->H * 4);
 }
 
-/* ProcessFrameWithPyramidDecomposition (.cs:145-206) */
+/* ProcessFrameWithPyramidDecomposition (.cs:145-206); with c->standard the
+ * spectral step is ProcessFrameWithStandardMagnification's (.cs:208-232) */
 static void process_pyramid(mm_ref *c, const float *in, float *out, mm_ref_dbg *dbg)
 {
     const int W = c->W, H = c->H, N = c->N, L = c->levels;
@@ -486,9 +544,28 @@ static void process_pyramid(mm_ref *c, const float *in, float *out, mm_ref_dbg *
     for (size_t p = 0; p < nn; ++p) ybuf[p] = pad_prev[p * 4];
     mm_ref_fft_centered(N, ybuf, (float *)Fp);             /* :156 */
 
+    const float S = c->phase_scale, tau = c->tau;
+    if (c->standard) {
+        /* ProcessPhaseDifferenceWithComputeShader (.cs:489-506) ->
+         * ProcessPhaseDifference (PhaseDifferenceComputeShader.compute:124-179) */
+        #pragma omp parallel for schedule(static)
+        for (int y = 0; y < N; ++y)
+            for (int x = 0; x < N; ++x) {
+                size_t p = (size_t)y * N + x;
+                cplx cur = Fc[p], prv = Fp[p];
+                float cm = sqrtf(cur.x * cur.x + cur.y * cur.y);
+                float pm = sqrtf(prv.x * prv.x + prv.y * prv.y);
+                if (cm < tau || pm < tau) { acc[p] = cur; continue; }      /* :140-146 */
+                float d = mm_ref_normalize_phase(atan2f(prv.y, prv.x) - atan2f(cur.y, cur.x));
+                float w = bandpass_weight(spatial_frequency(x, y, N), c->bp_apply, c->bp_low,
+                                          c->bp_high, c->bp_steep, c->bp_sens, c->bp_edge);
+                float md = (d * w) * S;                                      /* :158-165 */
+                cplx e = {cosf(md), sinf(md)};
+                acc[p] = cmul(cur, e);                                       /* :171-174 */
+            }
+    } else {
     /* :158-194 — ApplyPyramidFilter x2, phase difference, accumulate (per level,
      * in level order, accumulator initialised to 0: PyramidOperations:131-138) */
-    const float S = c->phase_scale, tau = c->tau;
     #pragma omp parallel for schedule(static)
     for (size_t p = 0; p < nn; ++p) {
         cplx a = {0.0f, 0.0f};
@@ -517,6 +594,7 @@ static void process_pyramid(mm_ref *c, const float *in, float *out, mm_ref_dbg *
             a.y += o.y;
         }
         acc[p] = a;
+    }
     }
     if (dbg && dbg->F_cur) memcpy(dbg->F_cur, Fc, sizeof(cplx) * nn);
     if (dbg && dbg->F_prev) memcpy(dbg->F_prev, Fp, sizeof(cplx) * nn);
@@ -568,7 +646,7 @@ void mm_ref_process(mm_ref *c, const float *in, float *out, mm_ref_dbg *dbg)
         c->first = 0;
         return;
     }
-    if (c->apply) process_pyramid(c, in, out, dbg);        /* :126-136 */
+    if (c->apply) process_pyramid(c, in, out, dbg);        /* :126-136 (both modes) */
     else memcpy(out, in, sizeof(float) * px);              /* :139 */
     memcpy(c->prev, in, sizeof(float) * px);               /* :142 */
 }

@@ -48,6 +48,19 @@ int     mm_ref_padded_size(const mm_ref *ctx);
 void    mm_ref_set_params(mm_ref *ctx, int levels, float min_freq, float max_freq,
                           float phase_scale, float mag_threshold, int edge_mode);
 void    mm_ref_set_apply(mm_ref *ctx, int apply_magnification);
+/* usePyramidDecomposition = false (.cs:18, :128-135): standard mode with the
+ * phase-delta band-pass of PhaseDifferenceComputeShader.compute (.cs:33-43,
+ * :489-506).  `edge_enhancement` is the value the component passes:
+ * enhanceEdges ? edgeEnhancement : 0 (.cs:504). */
+void    mm_ref_set_standard(mm_ref *ctx, int use_standard, int apply_bandpass,
+                            float low_cutoff, float high_cutoff, float steepness,
+                            float motion_sensitivity, float edge_enhancement);
+/* calculate_spatial_frequency + calculate_bandpass_weight
+ * (PhaseDifferenceComputeShader.compute:74-122) on the centred N*N grid. */
+void    mm_ref_bandpass_weights(int n, int apply_bandpass, float low_cutoff,
+                                float high_cutoff, float steepness,
+                                float motion_sensitivity, float edge_enhancement,
+                                float *out);
 void    mm_ref_reset(mm_ref *ctx);                 /* isFirstFrame = true */
 /* State = previousSourceTexture (W*H*4 floats) + first-frame flag. */
 size_t  mm_ref_state_size(const mm_ref *ctx);

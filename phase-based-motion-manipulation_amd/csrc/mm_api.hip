@@ -138,6 +138,17 @@ static void build_tab(int S, int N, int edge, std::vector<Tap4> &tab)
 static void build_spec(const mm_params &p, int N, Spec &sp)
 {
     memset(&sp, 0, sizeof(sp));
+    sp.mode = p.mode;
+    // standard mode: ProcessPhaseDifferenceWithComputeShader uniforms (.cs:489-506)
+    sp.bp_apply = p.apply_bandpass_filter ? 1 : 0;
+    sp.bp_low = p.low_frequency_cutoff;
+    sp.bp_high = p.high_frequency_cutoff;
+    sp.bp_steep = p.filter_steepness;
+    sp.bp_sens = p.motion_sensitivity;
+    sp.bp_edge = p.enhance_edges ? p.edge_enhancement : 0.0f;      // .cs:504
+    sp.bp_inv_low = 1.0f / fmaxf(p.low_frequency_cutoff, 0.001f);
+    sp.bp_inv_1mhigh = 1.0f / fmaxf(1.0f - p.high_frequency_cutoff, 0.001f);
+    sp.bp_inv_band = 1.0f / (p.high_frequency_cutoff - p.low_frequency_cutoff);
     sp.L = p.levels;
     sp.minF = p.min_freq;
     sp.maxF = p.max_freq;
@@ -178,7 +189,7 @@ static int validate_params(const mm_params *p)
     if (!p) return MM_ERR_INVALID;
     if (p->levels < 1 || p->levels > kMaxLevels) return MM_ERR_UNSUPPORTED;
     if (p->orientations != 1) return MM_ERR_UNSUPPORTED;
-    if (p->mode != MM_MODE_PYRAMID) return MM_ERR_UNSUPPORTED;
+    if (p->mode != MM_MODE_PYRAMID && p->mode != MM_MODE_STANDARD) return MM_ERR_UNSUPPORTED;
     if (p->edge_mode != MM_EDGE_REPEAT && p->edge_mode != MM_EDGE_CLAMP) return MM_ERR_INVALID;
     if (!(p->min_freq > 0.0f) || !(p->max_freq > 0.0f)) return MM_ERR_INVALID;
     return MM_OK;
@@ -209,11 +220,11 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
     if (fmt == MM_RGBA8)
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+                           2 * lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
                            h->d_row3, h->d_tw, h->d_G, h->g_stride);
     else
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+                           2 * lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
                            h->d_row3, h->d_tw, h->d_G, h->g_stride);
     HIPCHK(hipGetLastError());
     return MM_OK;
@@ -228,9 +239,16 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     const int blocks = (cols + gpw - 1) / gpw;
     ProfScope ps(h, s, MM_K_COLS, nframes);
     // two LDS areas per group: FFT exchange + the packed (0, N/2) column pair's A
-    hipLaunchKernelGGL((k_cols<LOG2N>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                       2 * lds_fft_bytes<LOG2N>(), s, h->d_G, h->g_stride, h->d_Q, h->q_stride,
-                       st_in, st_out, nframes, first_passthrough, h->geo, h->spec, h->d_tw);
+    if (h->spec.mode == MM_MODE_STANDARD)
+        hipLaunchKernelGGL((k_cols<LOG2N, MM_MODE_STANDARD>), dim3(blocks),
+                           dim3(wg_threads<LOG2N>()), 2 * lds_fft_bytes<LOG2N>(), s, h->d_G,
+                           h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,
+                           first_passthrough, h->geo, h->spec, h->d_tw);
+    else
+        hipLaunchKernelGGL((k_cols<LOG2N, MM_MODE_PYRAMID>), dim3(blocks),
+                           dim3(wg_threads<LOG2N>()), 2 * lds_fft_bytes<LOG2N>(), s, h->d_G,
+                           h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,
+                           first_passthrough, h->geo, h->spec, h->d_tw);
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -383,6 +401,13 @@ int mm_params_default(mm_params *p)
     p->mode = MM_MODE_PYRAMID;
     p->edge_mode = MM_EDGE_REPEAT;
     p->apply_magnification = 1;    // .cs:12
+    p->apply_bandpass_filter = 1;  // .cs:35
+    p->low_frequency_cutoff = 0.05f;
+    p->high_frequency_cutoff = 0.4f;
+    p->filter_steepness = 3.0f;
+    p->motion_sensitivity = 1.5f;  // .cs:41
+    p->enhance_edges = 1;
+    p->edge_enhancement = 0.8f;    // .cs:43
     return MM_OK;
 }
 

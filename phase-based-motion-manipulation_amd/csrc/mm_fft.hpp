@@ -92,7 +92,7 @@ __device__ __forceinline__ c2 pass_twiddle(int t, int q, const c2 *__restrict__ 
     return twiddle<DIR>(tw, ((t + q * T) & (NS - 1)) * TWS);
 }
 
-template <int N, int R, int NS, int DIR, bool LAST>
+template <int N, int R, int NS, int DIR, bool LAST, bool DB>
 __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *wb)
 {
     constexpr int T = N / 8;
@@ -137,7 +137,10 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *w
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = lds[pad8(t + j * T)];
-        __syncthreads();
+        // Double-buffered (DB): the next exchange writes the other buffer, and a
+        // buffer is rewritten only after everyone passed the barrier that follows
+        // its reads -- so no second barrier here.
+        if (!DB) __syncthreads();
     }
 }
 
@@ -162,24 +165,45 @@ __device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *
     }
 }
 
-template <int LOG2N, int DIR, int P, int NS>
-__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+template <int LOG2N, int DIR, int P, int NS, bool DB>
+__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds0, c2 *lds1,
+                                              const c2 (&wb)[16])
 {
     if constexpr (P < fft_passes<LOG2N>()) {
         constexpr int R = pass_radix<LOG2N, P>();
-        fft_pass<(1 << LOG2N), R, NS, DIR, P == fft_passes<LOG2N>() - 1>(v, t, lds, wb + P * 4);
-        fft_pass_loop<LOG2N, DIR, P + 1, NS * R>(v, t, lds, wb);
+        c2 *lds = (DB && (P & 1)) ? lds1 : lds0;
+        fft_pass<(1 << LOG2N), R, NS, DIR, P == fft_passes<LOG2N>() - 1, DB>(v, t, lds, wb + P * 4);
+        fft_pass_loop<LOG2N, DIR, P + 1, NS * R, DB>(v, t, lds0, lds1, wb);
     }
 }
 
+// LDS exchanges of one FFT; with double buffering, exchange e uses buffer e & 1
+// (relative to the buffers passed in) and the LAST one leaves its buffer
+// "dirty" (slower threads may still read it until the caller's next barrier).
+template <int LOG2N> constexpr int fft_exchanges() { return fft_passes<LOG2N>() - 1; }
+template <int LOG2N> constexpr int fft_dirty_buffer() { return (fft_exchanges<LOG2N>() - 1) & 1; }
+
 // Unnormalised DFT of the group's sequence, DIR=-1 forward, DIR=+1 inverse.
 // Every thread of the WORKGROUP must call this (it contains __syncthreads).
+// Single-buffered form: ends with a barrier, LDS free on return.
 template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
 {
     c2 wb[16];
     preload_twiddles<LOG2N, DIR, 0, 1>(wb, t, tw);
-    fft_pass_loop<LOG2N, DIR, 0, 1>(v, t, lds, wb);
+    fft_pass_loop<LOG2N, DIR, 0, 1, false>(v, t, lds, lds, wb);
+}
+
+// Double-buffered form over (b0, b1): one barrier per exchange.  On return the
+// buffer fft_dirty_buffer() (0 -> b0, 1 -> b1) may still be read by other
+// threads; the other one is free.
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void fft_regs_db(c2 (&v)[8], int t, c2 *b0, c2 *b1,
+                                            const c2 *__restrict__ tw)
+{
+    c2 wb[16];
+    preload_twiddles<LOG2N, DIR, 0, 1>(wb, t, tw);
+    fft_pass_loop<LOG2N, DIR, 0, 1, true>(v, t, b0, b1, wb);
 }
 
 }  // namespace mm

@@ -38,6 +38,11 @@ struct Geo {
 };
 
 struct Spec {
+    int mode;               // MM_MODE_PYRAMID (0) | MM_MODE_STANDARD (1)
+    // standard mode band-pass (PhaseDifferenceComputeShader.compute:88-122)
+    int bp_apply;
+    float bp_low, bp_high, bp_steep, bp_sens, bp_edge;
+    float bp_inv_low, bp_inv_1mhigh, bp_inv_band;
     int L;
     float minF, maxF, S, tau2, inv_nn;
     float hp_lo, hp_inv;    // high-pass ramp start maxF*0.8, 1/(maxF*0.2)
@@ -283,7 +288,41 @@ __device__ __forceinline__ c2 pyramid_op(c2 c, c2 p, int fx, int fy, const Spec 
 // grid is then exactly N/2 groups (1024 at N=2048: one resident round at 4
 // WGs/CU instead of 1025 with a one-WG tail).  Column N/2's F_{t-1} lives in the
 // state buffer between frames.
+// ProcessPhaseDifference (PhaseDifferenceComputeShader.compute:124-179) for one
+// bin of the unmasked spectrum (standard mode, .cs:208-232):
+//   A = c * e^{i S w(sf) wrap(arg p - arg c)} / N^2, or c / N^2 if |c| or |p| < tau,
+// w = calculate_bandpass_weight(calculate_spatial_frequency) (:74-122).
 template <int LOG2N>
+__device__ __forceinline__ c2 standard_op(c2 c, c2 p, int fx, int fy, const Spec &sp)
+{
+    constexpr int N = 1 << LOG2N;
+    const float ux = (float)fx * (1.0f / (float)N);
+    const float uy = (float)(fy <= N / 2 ? fy : N - fy) * (1.0f / (float)N);
+    const float sf = fminf(__builtin_amdgcn_sqrtf(ux * ux + uy * uy) / 0.707f, 1.0f);
+    const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
+    if (mn2 < sp.tau2) return scale(c, sp.inv_nn);
+    float w = 1.0f;
+    if (sp.bp_apply) {
+        if (sf < sp.bp_low) w *= __powf(sf * sp.bp_inv_low, sp.bp_steep);
+        if (sf > sp.bp_high) w *= __powf((1.0f - sf) * sp.bp_inv_1mhigh, sp.bp_steep);
+        w *= sp.bp_sens;
+        if (sf > sp.bp_low && sf < sp.bp_high)
+            w *= 1.0f + sp.bp_edge * __sinf(kPi * (sf - sp.bp_low) * sp.bp_inv_band);
+        w = fmaxf(w, 0.0f);
+    }
+    const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
+    const float ph = (d * w) * sp.S;
+    return scale(mul(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
+}
+
+template <int LOG2N, int MODE>
+__device__ __forceinline__ c2 spectral_op(c2 c, c2 p, int fx, int fy, const Spec &sp)
+{
+    if constexpr (MODE == 0) return pyramid_op<LOG2N>(c, p, fx, fy, sp);
+    else return standard_op<LOG2N>(c, p, fx, fy, sp);
+}
+
+template <int LOG2N, int MODE>
 __global__ __launch_bounds__(wg_threads<LOG2N>())
 void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_t q_stride,
             const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
@@ -344,8 +383,8 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
                 const c2 fN = mk(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
                 if (!pass_frame && fy <= N / 2) {
                     const c2 pn = pNsrc ? pNsrc[fy] : mk(0.0f, 0.0f);
-                    A0[fy] = pyramid_op<LOG2N>(f0, prev[j], 0, fy, sp);
-                    AN[fy] = pyramid_op<LOG2N>(fN, pn, N / 2, fy, sp);
+                    A0[fy] = spectral_op<LOG2N, MODE>(f0, prev[j], 0, fy, sp);
+                    AN[fy] = spectral_op<LOG2N, MODE>(fN, pn, N / 2, fy, sp);
                 }
                 prev[j] = f0;
                 stN[fy] = fN;
@@ -382,7 +421,7 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
             for (int j = 0; j < 8; ++j) {
                 // one bin at a time: keeps the 8 op instances from being interleaved
                 __builtin_amdgcn_sched_barrier(0);
-                const c2 a = pyramid_op<LOG2N>(v[j], prev[j], f, t + j * T, sp);
+                const c2 a = spectral_op<LOG2N, MODE>(v[j], prev[j], f, t + j * T, sp);
                 prev[j] = v[j];
                 v[j] = a;
             }

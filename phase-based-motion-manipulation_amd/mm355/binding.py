@@ -15,6 +15,7 @@ RGBA32F = 1
 EDGE_REPEAT = 0
 EDGE_CLAMP = 1
 MODE_PYRAMID = 0
+MODE_STANDARD = 1
 FRAMES_ON_DEVICE = 1
 
 KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv", "k_compose")   # MM_K_* ids 0..3
@@ -36,27 +37,42 @@ class Params(ctypes.Structure):
                 ("max_freq", ctypes.c_float), ("phase_scale", ctypes.c_float),
                 ("magnitude_threshold", ctypes.c_float), ("orientations", ctypes.c_int),
                 ("mode", ctypes.c_int), ("edge_mode", ctypes.c_int),
-                ("apply_magnification", ctypes.c_int)]
+                ("apply_magnification", ctypes.c_int),
+                ("apply_bandpass_filter", ctypes.c_int), ("low_frequency_cutoff", ctypes.c_float),
+                ("high_frequency_cutoff", ctypes.c_float), ("filter_steepness", ctypes.c_float),
+                ("motion_sensitivity", ctypes.c_float), ("enhance_edges", ctypes.c_int),
+                ("edge_enhancement", ctypes.c_float)]
 
     @classmethod
     def make(cls, levels=5, min_freq=0.05, max_freq=0.45, phase_scale=10.0,
-             magnitude_threshold=0.01, edge_mode=EDGE_REPEAT, apply_magnification=True):
+             magnitude_threshold=0.01, edge_mode=EDGE_REPEAT, apply_magnification=True,
+             mode=MODE_PYRAMID, **standard):
+        """standard-mode fields (mm.h) by keyword: apply_bandpass_filter,
+        low_frequency_cutoff, high_frequency_cutoff, filter_steepness,
+        motion_sensitivity, enhance_edges, edge_enhancement."""
         p = cls()
         lib().mm_params_default(ctypes.byref(p))
         p.levels, p.min_freq, p.max_freq = levels, min_freq, max_freq
         p.phase_scale, p.magnitude_threshold = phase_scale, magnitude_threshold
         p.edge_mode, p.apply_magnification = edge_mode, 1 if apply_magnification else 0
+        p.mode = mode
+        for k, v in standard.items():
+            if k not in dict(cls._fields_):
+                raise TypeError(f"unknown mm_params field {k}")
+            setattr(p, k, int(v) if k in ("apply_bandpass_filter", "enhance_edges") else v)
         return p
 
 
 _lib = None
 
 
-def load_library(path=LIB_PATH):
-    """Load the HIP product library; raises if it is missing (no fallback)."""
+def load_library(path=None):
+    """Load the HIP product library; raises if it is missing (no fallback).
+    MM355_LIB overrides the path (A/B builds of the same library)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("MM355_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise MMError(-3, f"HIP library not built: {path} (run __graft_entry__.build())")
     L = ctypes.CDLL(path)

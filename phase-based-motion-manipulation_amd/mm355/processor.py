@@ -6,7 +6,8 @@ snake_case; methods keep the reference's Unity callback names.
 """
 import numpy as np
 
-from .binding import (EDGE_REPEAT, RGBA8, RGBA32F, Handle, MMError, Params)
+from .binding import (EDGE_REPEAT, MODE_PYRAMID, MODE_STANDARD, RGBA8, RGBA32F, Handle,
+                      MMError, Params)
 
 
 def _fmt_of(frame):
@@ -32,8 +33,10 @@ class MotionMagnificationProcessor:
     def __init__(self, width, height, *, apply_motion_magnification=True,
                  show_magnitude=False, show_phase=False, use_pyramid_decomposition=True,
                  pyramid_levels=5, min_frequency=0.05, max_frequency=0.45,
-                 phase_scale=10.0, magnitude_threshold=0.01, edge_mode=EDGE_REPEAT,
-                 device=0):
+                 phase_scale=10.0, magnitude_threshold=0.01, apply_bandpass_filter=True,
+                 low_frequency_cutoff=0.05, high_frequency_cutoff=0.4, filter_steepness=3.0,
+                 motion_sensitivity=1.5, enhance_edges=True, edge_enhancement=0.8,
+                 edge_mode=EDGE_REPEAT, device=0):
         self.width, self.height, self.device = width, height, device
         self.apply_motion_magnification = apply_motion_magnification  # .cs:12
         self.show_magnitude = show_magnitude                          # .cs:13
@@ -44,21 +47,35 @@ class MotionMagnificationProcessor:
         self.max_frequency = max_frequency                            # .cs:21
         self.phase_scale = phase_scale                                # .cs:29
         self.magnitude_threshold = magnitude_threshold                # .cs:30
+        self.apply_bandpass_filter = apply_bandpass_filter            # .cs:35
+        self.low_frequency_cutoff = low_frequency_cutoff              # .cs:36
+        self.high_frequency_cutoff = high_frequency_cutoff            # .cs:37
+        self.filter_steepness = filter_steepness                      # .cs:38
+        self.motion_sensitivity = motion_sensitivity                  # .cs:41
+        self.enhance_edges = enhance_edges                            # .cs:42
+        self.edge_enhancement = edge_enhancement                      # .cs:43
         self.edge_mode = edge_mode
         self._handle = None
 
     # -- reference lifecycle -------------------------------------------------
     def _params(self):
-        if not self.use_pyramid_decomposition:
-            # ProcessFrameWithStandardMagnification (.cs:208-232): not built yet
-            raise MMError(-2, "use_pyramid_decomposition=False (standard mode)")
         if self.show_magnitude or self.show_phase:
             raise MMError(-2, "debug views (.cs:234-257) are out of scope")
+        # usePyramidDecomposition selects ProcessFrameWithPyramidDecomposition or
+        # ProcessFrameWithStandardMagnification (.cs:128-135)
+        mode = MODE_PYRAMID if self.use_pyramid_decomposition else MODE_STANDARD
         return Params.make(levels=self.pyramid_levels, min_freq=self.min_frequency,
                            max_freq=self.max_frequency, phase_scale=self.phase_scale,
                            magnitude_threshold=self.magnitude_threshold,
                            edge_mode=self.edge_mode,
-                           apply_magnification=self.apply_motion_magnification)
+                           apply_magnification=self.apply_motion_magnification, mode=mode,
+                           apply_bandpass_filter=self.apply_bandpass_filter,
+                           low_frequency_cutoff=self.low_frequency_cutoff,
+                           high_frequency_cutoff=self.high_frequency_cutoff,
+                           filter_steepness=self.filter_steepness,
+                           motion_sensitivity=self.motion_sensitivity,
+                           enhance_edges=self.enhance_edges,
+                           edge_enhancement=self.edge_enhancement)
 
     def Start(self):
         """Start -> InitializeProcessor (.cs:90-94, :289-342). Raises on failure."""

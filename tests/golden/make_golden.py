@@ -30,6 +30,10 @@ CASES = [
     ("wide_L5_S25", 200, 120, 5, 25.0, 0, False, 3, False),
     ("c1_256_gray_L3_S10", 256, 256, 3, 10.0, 0, True, 4, False),
 ]
+# standard (non-pyramid) mode cases (f1): name -> oracle set_standard() kwargs
+STANDARD = {"std_96x64_S25": (96, 64, 5, 25.0, 0, False, 3, False, {}),
+            "std_64x48_S9p7_steep2": (64, 48, 5, 9.7, 1, False, 3, False,
+                                       {"steep": 2.0, "high": 0.3})}
 
 
 def save(name, arr, manifest, entry):
@@ -46,10 +50,13 @@ def main():
     manifest = {"generator": "tests/golden/make_golden.py (CPU oracle, fp32)",
                 "seed": 0x5EED0000, "min_freq": 0.05, "max_freq": 0.45,
                 "magnitude_threshold": 0.01, "cases": {}}
-    for name, W, H, L, S, edge, gray, nf, dump in CASES:
+    cases = [c + (None,) for c in CASES] + [(k,) + v for k, v in STANDARD.items()]
+    for name, W, H, L, S, edge, gray, nf, dump, std in cases:
         frames = [O.synth_frame(W, H, t, gray=gray) for t in range(nf)]
         ff = [f.astype(np.float32) / np.float32(255) for f in frames]
         o = O.Oracle(W, H, levels=L, phase_scale=S, edge_mode=edge)
+        if std is not None:
+            o.set_standard(True, **std)
         outs, dbg = [], None
         for k, f in enumerate(ff):
             if dump and k == 1:
@@ -59,11 +66,13 @@ def main():
             outs.append(out)
         for k in range(1, nf):
             tw = np_twin.process_frame(ff[k].astype(np.float64), ff[k - 1].astype(np.float64),
-                                       L, 0.05, 0.45, S, edge=edge)
+                                       L, 0.05, 0.45, S, edge=edge, standard=std)
             err = float(np.abs(outs[k] - tw).max())
             assert err < 5e-6, (name, k, err)
         entry = {"width": W, "height": H, "levels": L, "phase_scale": S, "edge_mode": edge,
                  "gray": gray, "frames": nf}
+        if std is not None:
+            entry["standard"] = std
         save(f"{name}__inputs_u8", np.stack(frames), manifest, entry)
         out = np.stack(outs)
         if gray:   # R = G = B (to fp32 rounding), alpha = 1: keep R only

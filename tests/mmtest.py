@@ -17,19 +17,33 @@ def synth(W, H, n, t0=0, gray=False, seed=0x5EED0000, fmt="f32"):
     return [f.astype(np.float32) / np.float32(255.0) for f in fr]
 
 
-def oracle_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, apply=True):
+# standard-mode settings in oracle terms -> mm_params fields
+def _std_fields(std):
+    return dict(apply_bandpass_filter=std.get("apply", True),
+                low_frequency_cutoff=std.get("low", 0.05),
+                high_frequency_cutoff=std.get("high", 0.4),
+                filter_steepness=std.get("steep", 3.0),
+                motion_sensitivity=std.get("sens", 1.5),
+                enhance_edges=True, edge_enhancement=std.get("edge", 0.8))
+
+
+def oracle_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, apply=True,
+               standard=None):
     o = O.Oracle(W, H, levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
                  edge_mode=edge)
     o.set_apply(apply)
+    if standard is not None:
+        o.set_standard(True, **standard)
     return [o.process(f) for f in frames]
 
 
 def gpu_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, mode="frame",
-            apply=True):
+            apply=True, standard=None):
     import torch
     import mm355
+    extra = {} if standard is None else dict(mode=mm355.MODE_STANDARD, **_std_fields(standard))
     p = mm355.Params.make(levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
-                          edge_mode=edge, apply_magnification=apply)
+                          edge_mode=edge, apply_magnification=apply, **extra)
     h = mm355.Handle(W, H, p)
     fmt = mm355.RGBA8 if frames[0].dtype == np.uint8 else mm355.RGBA32F
     dev_in = torch.from_numpy(np.stack(frames)).cuda()

@@ -134,8 +134,29 @@ def blur(img, edge):
     return one(one(img, 1), 0)
 
 
-def process_frame(cur, prev, L, minf, maxf, S, tau=0.01, edge=0, dbg=None):
-    """One non-first OnRenderImage call on float RGBA frames [H, W, 4]."""
+def bandpass_weights(N, apply=True, low=0.05, high=0.4, steep=3.0, sens=1.5, edge=0.8):
+    """calculate_spatial_frequency + calculate_bandpass_weight
+    (PhaseDifferenceComputeShader.compute:74-122), float64."""
+    f1 = np.arange(N) / N - 0.5
+    FX, FY = np.meshgrid(f1, f1)
+    sf = np.minimum(np.sqrt(FX * FX + FY * FY) / np.float64(np.float32(0.707)), 1.0)
+    if not apply:
+        return np.ones_like(sf)
+    w = np.ones_like(sf)
+    lo = sf < low
+    w[lo] *= (sf[lo] / max(low, 0.001)) ** steep
+    hi = sf > high
+    w[hi] *= ((1.0 - sf[hi]) / max(1.0 - high, 0.001)) ** steep
+    w *= sens
+    mid = (sf > low) & (sf < high)
+    w[mid] *= 1.0 + edge * np.sin(PI * (sf[mid] - low) / (high - low))
+    return np.maximum(w, 0.0)
+
+
+def process_frame(cur, prev, L, minf, maxf, S, tau=0.01, edge=0, dbg=None, standard=None):
+    """One non-first OnRenderImage call on float RGBA frames [H, W, 4].
+    standard: None (pyramid mode) or dict of bandpass_weights() arguments
+    (ProcessFrameWithStandardMagnification, .cs:208-232)."""
     H, W = cur.shape[:2]
     N = next_pow2(max(W, H))
     pc = pad_window(cur, N, edge)
@@ -143,7 +164,12 @@ def process_frame(cur, prev, L, minf, maxf, S, tau=0.01, edge=0, dbg=None):
     Fc = np.fft.fftshift(np.fft.fft2(pc[..., 0]))
     Fp = np.fft.fftshift(np.fft.fft2(pp[..., 0]))
     acc = np.zeros_like(Fc)
-    for i, m in enumerate(masks(N, L, minf, maxf)):
+    if standard is not None:
+        gate = (np.abs(Fc) < tau) | (np.abs(Fp) < tau)
+        d = wrap_phase(np.angle(Fp) - np.angle(Fc))
+        w = bandpass_weights(N, **standard)
+        acc = np.where(gate, Fc, Fc * np.exp(1j * S * w * d))
+    for i, m in enumerate(masks(N, L, minf, maxf) if standard is None else []):
         c = Fc * m
         p = Fp * m
         if i == 0 or i == L - 1:

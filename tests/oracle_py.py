@@ -49,6 +49,9 @@ def lib():
         L.mm_ref_set_params.argtypes = [vp, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_int]
         L.mm_ref_set_apply.argtypes = [vp, ctypes.c_int]
+        cf = ctypes.c_float
+        L.mm_ref_set_standard.argtypes = [vp, ctypes.c_int, ctypes.c_int, cf, cf, cf, cf, cf]
+        L.mm_ref_bandpass_weights.argtypes = [ctypes.c_int, ctypes.c_int, cf, cf, cf, cf, cf, fp]
         L.mm_ref_reset.argtypes = [vp]
         L.mm_ref_state_size.restype = ctypes.c_size_t
         L.mm_ref_state_size.argtypes = [vp]
@@ -134,6 +137,12 @@ def yiq_to_rgb(yiq):
     return o
 
 
+def bandpass_weights(n, apply=True, low=0.05, high=0.4, steep=3.0, sens=1.5, edge=0.8):
+    out = np.empty((n, n), np.float32)
+    lib().mm_ref_bandpass_weights(n, 1 if apply else 0, low, high, steep, sens, edge, _fp(out))
+    return out
+
+
 def blur(img, edge=EDGE_REPEAT):
     a = np.ascontiguousarray(img, np.float32).copy()
     lib().mm_ref_blur(a.shape[0], edge, _fp(a))
@@ -167,6 +176,12 @@ class Oracle:
 
     def set_apply(self, on):
         lib().mm_ref_set_apply(self.h, 1 if on else 0)
+
+    def set_standard(self, on=True, apply=True, low=0.05, high=0.4, steep=3.0, sens=1.5,
+                     edge=0.8):
+        """usePyramidDecomposition = false; edge = enhanceEdges ? edgeEnhancement : 0."""
+        lib().mm_ref_set_standard(self.h, 1 if on else 0, 1 if apply else 0, low, high, steep,
+                                  sens, edge)
 
     def reset(self):
         lib().mm_ref_reset(self.h)

@@ -43,7 +43,7 @@ def test_generator_reproduces_inputs(case):
 def test_oracle_reproduces_outputs(case):
     c = MAN["cases"][case]
     outs = T.oracle_run(c["width"], c["height"], inputs_f32(case), c["levels"], c["phase_scale"],
-                        c["edge_mode"])
+                        c["edge_mode"], standard=c.get("standard"))
     ref = load(case, "outputs_f32")
     got = np.stack(outs)
     if c["gray"]:
@@ -69,7 +69,7 @@ def test_gpu_matches_golden(case):
     c = MAN["cases"][case]
     fr = inputs_f32(case)
     got = np.stack(T.gpu_run(c["width"], c["height"], fr, c["levels"], c["phase_scale"],
-                             c["edge_mode"], mode="stream"))
+                             c["edge_mode"], mode="stream", standard=c.get("standard")))
     ref = load(case, "outputs_f32")
     assert np.array_equal(got[0], fr[0])
     if c["gray"]:

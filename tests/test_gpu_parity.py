@@ -196,3 +196,43 @@ def test_chunk_boundary_state_handoff():
         assert np.array_equal(got[k], full[k]), k
     r0.close()
     r1.close()
+
+
+@pytest.mark.parametrize("W,H,S,std", [
+    (64, 48, 10.0, {}), (200, 120, 25.0, dict(steep=2.0, high=0.3)),
+    (128, 96, 9.7, dict(apply=False)), (96, 96, 25.0, dict(edge=0.0, sens=1.0))])
+def test_standard_mode_f32(W, H, S, std):
+    """f1: usePyramidDecomposition = false (ProcessFrameWithStandardMagnification)."""
+    fr = T.synth(W, H, 4)
+    ref = T.oracle_run(W, H, fr, S=S, standard=std)
+    got = T.gpu_run(W, H, fr, S=S, standard=std, mode="stream")
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r, integer_scale=float(S).is_integer())
+
+
+@pytest.mark.slow
+def test_standard_mode_1080p_u8():
+    W, H = 1920, 1080
+    fr = T.synth(W, H, 2, fmt="u8")
+    ref = T.oracle_run(W, H, fr, S=25.0, standard={})
+    got = T.gpu_run(W, H, fr, S=25.0, standard={})
+    T.assert_close_u8(got[1], ref[1])
+
+
+def test_processor_standard_mode():
+    import torch
+    import mm355
+    W, H = 64, 48
+    fr = T.synth(W, H, 3)
+    ref = T.oracle_run(W, H, fr, S=25.0, standard={})
+    proc = mm355.MotionMagnificationProcessor(W, H, phase_scale=25.0,
+                                              use_pyramid_decomposition=False).Start()
+    src = torch.from_numpy(np.stack(fr)).cuda()
+    dst = torch.empty_like(src)
+    for k in range(3):
+        proc.OnRenderImage(src[k], dst[k])
+    torch.cuda.synchronize()
+    for k in range(1, 3):
+        T.assert_close_f32(dst[k].cpu().numpy(), ref[k])
+    proc.OnDestroy()

@@ -171,3 +171,42 @@ def test_oracle_vs_float64_twin(W, H, L, S, gray, edge):
                                edge=edge)
     e = np.abs(a1 - b1)
     assert e.max() < 5e-6 and np.sqrt((e ** 2).mean()) < 1e-6
+
+
+# ---- standard (non-pyramid) mode, f1: PhaseDifferenceComputeShader.compute ----
+
+def test_bandpass_weights_known_values():
+    w = O.bandpass_weights(128)                      # defaults .cs:35-43
+    assert w[64, 64] == 0.0                          # DC: pow(0, steepness) = 0
+    assert abs(w.max() - 1.5 * 1.8) < 1e-3           # sens * (1 + edge) at the band centre
+    assert np.abs(w - np_twin.bandpass_weights(128)).max() < 1e-5
+    assert np.all(O.bandpass_weights(64, apply=False) == 1.0)
+
+
+@pytest.mark.parametrize("W,H,S,std", [
+    (64, 48, 10.0, {}), (200, 120, 25.0, dict(steep=2.0, high=0.3)),
+    (96, 96, 9.7, dict(apply=False)), (64, 48, 25.0, dict(edge=0.0, sens=1.0))])
+def test_standard_mode_vs_float64_twin(W, H, S, std):
+    o = O.Oracle(W, H, phase_scale=S)
+    o.set_standard(True, **std)
+    f0 = O.synth_frame(W, H, 0).astype(np.float32) / 255
+    f1 = O.synth_frame(W, H, 3).astype(np.float32) / 255
+    o.process(f0)
+    a = o.process(f1)
+    b = np_twin.process_frame(f1.astype(np.float64), f0.astype(np.float64), 5, 0.05, 0.45, S,
+                              standard=std)
+    e = np.abs(a - b)
+    assert e.max() < 5e-6 and np.sqrt((e ** 2).mean()) < 1e-6
+
+
+def test_standard_mode_static_scene_is_identity_spectrum():
+    """prev == cur: delta = 0, so A = F and the output is the unmagnified
+    reconstruction -- independent of phase scale and band-pass settings."""
+    f = O.synth_frame(64, 48, 2).astype(np.float32) / 255
+    outs = []
+    for S, std in ((1.0, {}), (25.0, dict(steep=1.0, sens=3.0))):
+        o = O.Oracle(64, 48, phase_scale=S)
+        o.set_standard(True, **std)
+        o.process(f)
+        outs.append(o.process(f))
+    assert np.abs(outs[0] - outs[1]).max() < 1e-6
