@@ -105,27 +105,76 @@ class GpuBackend:
                               stream=self._stream())
 
 
-def cpu_baseline(W, H, L, S, seconds):
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(W, H, L, S, seconds, standard=False):
     """The CPU oracle (literal restatement of the reference algorithm) on the
-    host cores, bounded sample of the same stream."""
+    host cores, bounded sample of the same stream (BASELINE.md CPU-baseline
+    plan: all-core and single-thread).  Returns (record, outputs) where
+    outputs are the oracle's RGBA8 frames 0..n, kept for the parity check."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
     import oracle_py as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
-    threads = O.set_threads(threads)
-    o = O.Oracle(W, H, levels=L, phase_scale=S)
-    o.process(O.synth_frame(W, H, 0))          # first frame: passthrough, excluded
-    n, t0 = 0, time.perf_counter()
-    while n < 30:
-        o.process(O.synth_frame(W, H, n + 1))
-        n += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    o.close()
-    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames (t=1..{n}) of the same {W}x{H} synthetic stream, "
-                      f"L={L}, S={S}, after the passthrough frame; literal fp32 C "
-                      f"restatement (radix-2, 2 forward FFTs/frame), OpenMP {threads} threads"}
+
+    def run(threads, max_frames, budget, keep):
+        threads = O.set_threads(threads)
+        o = O.Oracle(W, H, levels=L, phase_scale=S)
+        if standard:
+            o.set_standard(True)
+        outs = [o.process(O.synth_frame(W, H, 0))]    # passthrough, not timed
+        n, t0 = 0, time.perf_counter()
+        while n < max_frames:
+            y = o.process(O.synth_frame(W, H, n + 1))
+            if keep:
+                outs.append(y)
+            n += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        dt = time.perf_counter() - t0
+        o.close()
+        return threads, n, dt, (np.stack(outs) if keep else None)
+
+    all_threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    thr, n, dt, outs = run(all_threads, 30, seconds, True)
+    _, n1, dt1, _ = run(1, 30, seconds / 3, False)
+    rec = {"value": round(n / dt, 4), "unit": "frames/s", "cores": thr, "kind": "port",
+           "single_thread_value": round(n1 / dt1, 4), "single_thread_frames": n1,
+           "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+           "sample": f"{n} frames (t=1..{n}) of the same {W}x{H} synthetic RGBA8 stream "
+                     f"(seed 0x5EED0000), L={L}, S={S}, after the passthrough frame; literal "
+                     f"fp32 C restatement (radix-2, 2 forward FFTs/frame, per-level passes), "
+                     f"OpenMP {thr} threads; single-thread on t=1..{n1}"}
+    return rec, outs
+
+
+def parity_check(mm355, torch, params, W, H, ref, local):
+    """The oracle's frames 0..n (cpu_baseline) against a fresh handle on the
+    same synthetic frames generated on the device (SURVEY.md §8c RGBA8 bar:
+    exact except +-1 LSB on <= 0.1% of values; frame 0 bitwise)."""
+    import numpy as np
+    n = ref.shape[0]
+    h = mm355.Handle(W, H, params, device=local)
+    fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(fr)
+    st = torch.cuda.current_stream().cuda_stream
+    h.synth(fr, 0, n, seed=0x5EED0000, stream=st)
+    h.process_stream(fr, out, n, mm355.RGBA8, stream=st)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    h.close()
+    d = np.abs(got.astype(np.int16) - ref.astype(np.int16))
+    return {"frames": int(n), "first_frame_bitwise": bool(np.array_equal(got[0], ref[0])),
+            "max_abs_lsb": int(d.max()), "frac_values_off": float((d > 0).mean()),
+            "rmse_lsb": round(float(np.sqrt((d.astype(np.float64) ** 2).mean())), 5),
+            "bar": "max 1 LSB, <= 0.1% of values"}
 
 
 def main():
@@ -232,9 +281,11 @@ def main():
                                  f"{HBM_PEAK_GBPS * 1e9 / B:.0f} frames/s per GPU"},
         "kernels": kern,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(W, H, a.levels, a.phase_scale, a.cpu_seconds)
     h.close()
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"], ref = cpu_baseline(W, H, a.levels, a.phase_scale,
+                                                   a.cpu_seconds, a.standard)
+        result["parity_vs_oracle"] = parity_check(mm355, torch, params, W, H, ref, local)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

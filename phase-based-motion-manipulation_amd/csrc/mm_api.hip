@@ -19,7 +19,7 @@
 #include <vector>
 
 #include "../../include/mm.h"
-#include "mm_kernels.hpp"
+#include "mm_kernels_w.hpp"
 
 using namespace mm;
 
@@ -48,6 +48,8 @@ struct mm_handle {
     float *d_Yh;
     size_t g_stride, q_stride, yh_stride;  // elements per frame
     int chunk;                  // frames per K1/K2/K3 batch
+    int nsub;                   // K2 (wave form): sub-chunks per column and launch
+    bool k2_wave;               // K2 as one wave per column (k_cols_w), N = 512..2048
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
@@ -220,11 +222,11 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
     if (fmt == MM_RGBA8)
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           2 * lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
                            h->d_row3, h->d_tw, h->d_G, h->g_stride);
     else
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           2 * lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
                            h->d_row3, h->d_tw, h->d_G, h->g_stride);
     HIPCHK(hipGetLastError());
     return MM_OK;
@@ -238,6 +240,22 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     const int cols = (1 << LOG2N) / 2;   // f = 0 and f = N/2 share group 0 (k_cols)
     const int blocks = (cols + gpw - 1) / gpw;
     ProfScope ps(h, s, MM_K_COLS, nframes);
+    if constexpr (LOG2N >= 9 && LOG2N <= 11) {
+        if (h->k2_wave) {
+            const int nsub = std::max(1, std::min(h->nsub, nframes));
+            const dim3 grid((1 << LOG2N) / 2 * nsub);
+            if (h->spec.mode == MM_MODE_STANDARD)
+                hipLaunchKernelGGL((k_cols_w<LOG2N, MM_MODE_STANDARD>), grid, dim3(64), 0, s,
+                                   h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out,
+                                   nframes, first_passthrough, nsub, h->geo, h->spec, h->d_tw);
+            else
+                hipLaunchKernelGGL((k_cols_w<LOG2N, MM_MODE_PYRAMID>), grid, dim3(64), 0, s,
+                                   h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out,
+                                   nframes, first_passthrough, nsub, h->geo, h->spec, h->d_tw);
+            HIPCHK(hipGetLastError());
+            return MM_OK;
+        }
+    }
     // two LDS areas per group: FFT exchange + the packed (0, N/2) column pair's A
     if (h->spec.mode == MM_MODE_STANDARD)
         hipLaunchKernelGGL((k_cols<LOG2N, MM_MODE_STANDARD>), dim3(blocks),
@@ -523,6 +541,12 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
 
     const char *ch = getenv("MM_CHUNK");
     h->chunk = ch ? std::max(1, atoi(ch)) : (N >= 4096 ? 4 : 8);
+    const char *ns = getenv("MM_NSUB");
+    h->nsub = ns ? std::max(1, atoi(ns)) : 3;
+    // K2 form: workgroup-per-column k_cols (default; fastest measured) or
+    // wave-per-column k_cols_w (MM_K2=wave; parity-tested)
+    const char *k2 = getenv("MM_K2");
+    h->k2_wave = k2 && strcmp(k2, "wave") == 0;
     h->g_stride = (size_t)(N / 2 + 1) * height;
     h->q_stride = (size_t)(N / 2 + 1) * g.Hq;
     h->yh_stride = (size_t)g.Hn * width;
