@@ -50,6 +50,7 @@ struct mm_handle {
     int chunk;                  // frames per K1/K2/K3 batch
     int nsub;                   // K2 (wave form): sub-chunks per column and launch
     bool k2_wave;               // K2 as one wave per column (k_cols_w), N = 512..2048
+    bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
@@ -173,6 +174,20 @@ static void build_spec(const mm_params &p, int N, Spec &sp)
     }
 }
 
+// k_cols' pyramid table holds <= 2 middle-band masks per bin: true unless some
+// three bands share an open interval (ratio maxF/minF spread over few levels).
+static bool bands_fit_table(const Spec &sp)
+{
+    for (int a = 1; a < sp.L - 1; ++a)
+        for (int b = a + 1; b < sp.L - 1; ++b)
+            for (int c = b + 1; c < sp.L - 1; ++c) {
+                const float lo = fmaxf(sp.lo[a], fmaxf(sp.lo[b], sp.lo[c]));
+                const float hi = fminf(sp.hi[a], fminf(sp.hi[b], sp.hi[c]));
+                if (lo < hi) return false;   // NaN bands (L = 3) compare false
+            }
+    return true;
+}
+
 // GaussianBlur.shader:47-60 at _BlurSize 0.5 (.cs:427): bilinear taps at
 // +-0.6923 and +-1.6154 texels == a 5-tap FIR.
 static Blur5 build_blur()
@@ -256,17 +271,16 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
             return MM_OK;
         }
     }
-    // two LDS areas per group: FFT exchange + the packed (0, N/2) column pair's A
-    if (h->spec.mode == MM_MODE_STANDARD)
-        hipLaunchKernelGGL((k_cols<LOG2N, MM_MODE_STANDARD>), dim3(blocks),
-                           dim3(wg_threads<LOG2N>()), 2 * lds_fft_bytes<LOG2N>(), s, h->d_G,
-                           h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,
-                           first_passthrough, h->geo, h->spec, h->d_tw);
-    else
-        hipLaunchKernelGGL((k_cols<LOG2N, MM_MODE_PYRAMID>), dim3(blocks),
-                           dim3(wg_threads<LOG2N>()), 2 * lds_fft_bytes<LOG2N>(), s, h->d_G,
-                           h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,
-                           first_passthrough, h->geo, h->spec, h->d_tw);
+    // per group: FFT exchange buffer + two per-bin tables (k_cols)
+    const size_t lds = k2_lds_bytes<LOG2N>();
+#define MM_K2_LAUNCH(MODE)                                                                 \
+    hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(wg_threads<LOG2N>()), lds, s, \
+                       h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,       \
+                       first_passthrough, h->geo, h->spec, h->d_tw)
+    if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
+    else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB);
+    else MM_K2_LAUNCH(MM_MODE_PYRAMID);
+#undef MM_K2_LAUNCH
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -537,6 +551,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.Hq = (g.Hn + 1) & ~1;
     g.edge = p->edge_mode;
     build_spec(*p, N, h->spec);
+    h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->blur = build_blur();
 
     const char *ch = getenv("MM_CHUNK");
@@ -599,6 +614,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     h->p = *p;
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
+    h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     if (edge_changed) return upload_tables(h);
     return MM_OK;
 }

@@ -16,22 +16,43 @@
 
 namespace mm {
 
+// Complex value.  Scalar FP32 on purpose: as a 2-wide vector the complex math
+// lowers to v_pk_*_f32, which on gfx950 measured SLOWER per frame than the
+// scalar form in these VALU-issue-bound kernels (k_cols 15.5 vs 13.9 us/frame
+// with 19% fewer VALU instructions), besides costing registers.
 struct c2 { float x, y; };
 
-__device__ __forceinline__ c2 mk(float x, float y) { c2 r; r.x = x; r.y = y; return r; }
+__host__ __device__ __forceinline__ c2 mk(float x, float y) { c2 r; r.x = x; r.y = y; return r; }
 __device__ __forceinline__ c2 add(c2 a, c2 b) { return mk(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ c2 sub(c2 a, c2 b) { return mk(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ c2 mul(c2 a, c2 b)
+__device__ __forceinline__ c2 operator+(c2 a, c2 b) { return add(a, b); }
+__device__ __forceinline__ c2 operator-(c2 a, c2 b) { return sub(a, b); }
+__device__ __forceinline__ c2 operator*(c2 a, float s) { return mk(a.x * s, a.y * s); }
+// x + i*DIR*y and x - i*DIR*y
+template <int DIR>
+__device__ __forceinline__ c2 add_i(c2 x, c2 y)
 {
-    return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    return DIR < 0 ? mk(x.x + y.y, x.y - y.x) : mk(x.x - y.y, x.y + y.x);
 }
-__device__ __forceinline__ c2 scale(c2 a, float s) { return mk(a.x * s, a.y * s); }
+template <int DIR>
+__device__ __forceinline__ c2 sub_i(c2 x, c2 y)
+{
+    return DIR < 0 ? mk(x.x - y.y, x.y + y.x) : mk(x.x + y.y, x.y - y.x);
+}
 // multiply by i*DIR  (DIR = -1 forward -> -i ; DIR = +1 inverse -> +i)
 template <int DIR>
 __device__ __forceinline__ c2 mul_i(c2 a)
 {
     return DIR < 0 ? mk(a.y, -a.x) : mk(-a.y, a.x);
 }
+__device__ __forceinline__ c2 mul(c2 a, c2 b)
+{
+    return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// the packed-form signature, kept for the shared butterfly code (wp unused)
+__device__ __forceinline__ c2 mul_p(c2 a, c2 w, c2) { return mul(a, w); }
+__device__ __forceinline__ c2 prime(c2 w) { return w; }
+__device__ __forceinline__ c2 scale(c2 a, float s) { return mk(a.x * s, a.y * s); }
 
 // LDS index padding: one complex every 8 (bank-conflict-free Stockham writes
 // for Ns = 1 and Ns = 8 with ds_write_b64).
@@ -49,30 +70,70 @@ __device__ __forceinline__ void dft2(c2 &a, c2 &b)
 template <int DIR>
 __device__ __forceinline__ void dft4(c2 &x0, c2 &x1, c2 &x2, c2 &x3)
 {
-    c2 s0 = add(x0, x2), d0 = sub(x0, x2);
-    c2 s1 = add(x1, x3), d1 = mul_i<DIR>(sub(x1, x3));
-    x0 = add(s0, s1);
-    x2 = sub(s0, s1);
-    x1 = add(d0, d1);
-    x3 = sub(d0, d1);
+    const c2 s0 = x0 + x2, d0 = x0 - x2;
+    const c2 s1 = x1 + x3, t = x1 - x3;
+    x0 = s0 + s1;
+    x2 = s0 - s1;
+    x1 = add_i<DIR>(d0, t);
+    x3 = sub_i<DIR>(d0, t);
 }
 
 template <int DIR>
 __device__ __forceinline__ void dft8(c2 *v)
 {
-    const float h = 0.70710678118654752f;
-    c2 a0 = add(v[0], v[4]), b0 = sub(v[0], v[4]);
-    c2 a1 = add(v[1], v[5]), b1 = sub(v[1], v[5]);
-    c2 a2 = add(v[2], v[6]), b2 = sub(v[2], v[6]);
-    c2 a3 = add(v[3], v[7]), b3 = sub(v[3], v[7]);
-    // b[n] *= W8^n, W8 = exp(DIR*i*pi/4)
-    b1 = mk(h * (b1.x - DIR * b1.y), h * (b1.y + DIR * b1.x));
-    b2 = mul_i<DIR>(b2);
-    b3 = mk(h * (-b3.x - DIR * b3.y), h * (-b3.y + DIR * b3.x));
+    constexpr float h = 0.70710678118654752f;
+    c2 a0 = v[0] + v[4], b0 = v[0] - v[4];
+    c2 a1 = v[1] + v[5], b1 = v[1] - v[5];
+    c2 a2 = v[2] + v[6], b2 = v[2] - v[6];
+    c2 a3 = v[3] + v[7], b3 = v[3] - v[7];
+    // b[n] *= W8^n, W8 = exp(DIR*i*pi/4) = (h, DIR h); W8^2 = i*DIR folds into
+    // the DFT4 below, W8^3 = i*DIR*W8
+    b1 = mul_p(b1, c2{h, DIR * h}, c2{-DIR * h, h});
+    b3 = mul_p(b3, c2{-h, DIR * h}, c2{-DIR * h, -h});
     dft4<DIR>(a0, a1, a2, a3);
-    dft4<DIR>(b0, b1, b2, b3);
+    // DFT4 of (b0, b1, i DIR b2, b3)
+    const c2 s0 = add_i<DIR>(b0, b2), d0 = sub_i<DIR>(b0, b2);
+    const c2 s1 = b1 + b3, t = b1 - b3;
     v[0] = a0; v[2] = a1; v[4] = a2; v[6] = a3;
-    v[1] = b0; v[3] = b1; v[5] = b2; v[7] = b3;
+    v[1] = s0 + s1;
+    v[5] = s0 - s1;
+    v[3] = add_i<DIR>(d0, t);
+    v[7] = sub_i<DIR>(d0, t);
+}
+
+// u[m] *= w^m (m < R, R <= 16), powers by products of the base w (<= 4
+// roundings).  Every product and every multiply is mul_p (2 packed ops) with
+// the primed operand computed once.
+template <int R>
+__device__ __forceinline__ void apply_twiddles(c2 *u, c2 w1)
+{
+    const c2 p1 = prime(w1);
+    if constexpr (R >= 2) u[1] = mul_p(u[1], w1, p1);
+    if constexpr (R >= 4) {
+        const c2 w2 = mul_p(w1, w1, p1), p2 = prime(w2);
+        const c2 w3 = mul_p(w2, w1, p1);
+        u[2] = mul_p(u[2], w2, p2);
+        u[3] = mul(u[3], w3);
+        if constexpr (R >= 8) {
+            const c2 w4 = mul_p(w2, w2, p2), p4 = prime(w4);
+            u[4] = mul_p(u[4], w4, p4);
+            u[5] = mul(u[5], mul_p(w1, w4, p4));
+            u[6] = mul(u[6], mul_p(w2, w4, p4));
+            u[7] = mul(u[7], mul_p(w3, w4, p4));
+            if constexpr (R >= 16) {
+                const c2 w8 = mul_p(w4, w4, p4), p8 = prime(w8);
+                u[8] = mul_p(u[8], w8, p8);
+                u[9] = mul(u[9], mul_p(w1, w8, p8));
+                u[10] = mul(u[10], mul_p(w2, w8, p8));
+                u[11] = mul(u[11], mul_p(w3, w8, p8));
+                const c2 w12 = mul_p(w4, w8, p8), p12 = prime(w12);
+                u[12] = mul_p(u[12], w12, p12);
+                u[13] = mul(u[13], mul_p(w1, w12, p12));
+                u[14] = mul(u[14], mul_p(w2, w12, p12));
+                u[15] = mul(u[15], mul_p(w3, w12, p12));
+            }
+        }
+    }
 }
 
 // Twiddle W_N^idx from the device table tw[idx] = exp(-2*pi*i*idx/N).
@@ -104,23 +165,7 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *w
         c2 u[R];
 #pragma unroll
         for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
-        if (NS > 1) {
-            // base twiddle preloaded at FFT start; W^m by products (<= 3 roundings)
-            c2 w[R];
-            w[1] = wb[q];
-            if (R >= 4) {
-                w[2] = mul(w[1], w[1]);
-                w[3] = mul(w[2], w[1]);
-            }
-            if (R == 8) {
-                w[4] = mul(w[2], w[2]);
-                w[5] = mul(w[4], w[1]);
-                w[6] = mul(w[4], w[2]);
-                w[7] = mul(w[4], w[3]);
-            }
-#pragma unroll
-            for (int m = 1; m < R; ++m) u[m] = mul(u[m], w[m]);
-        }
+        if (NS > 1) apply_twiddles<R>(u, wb[q]);   // base preloaded at FFT start
         if (R == 8) dft8<DIR>(u);
         else if (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
         else dft2<DIR>(u[0], u[1]);

@@ -281,13 +281,6 @@ __device__ __forceinline__ c2 pyramid_op(c2 c, c2 p, int fx, int fy, const Spec 
     return a;
 }
 
-// Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
-// f = N/2 (row DFT bins that are real for real rows, so their column spectra are
-// Hermitian in fy) share group 0 of block 0 as one complex column z = G0 + i*GN:
-// the pyramid op runs on fy <= N/2 for both and the upper half is mirrored.  The
-// grid is then exactly N/2 groups (1024 at N=2048: one resident round at 4
-// WGs/CU instead of 1025 with a one-WG tail).  Column N/2's F_{t-1} lives in the
-// state buffer between frames.
 // ProcessPhaseDifference (PhaseDifferenceComputeShader.compute:124-179) for one
 // bin of the unmasked spectrum (standard mode, .cs:208-232):
 //   A = c * e^{i S w(sf) wrap(arg p - arg c)} / N^2, or c / N^2 if |c| or |p| < tau,
@@ -322,22 +315,145 @@ __device__ __forceinline__ c2 spectral_op(c2 c, c2 p, int fx, int fy, const Spec
     else return standard_op<LOG2N>(c, p, fx, fy, sp);
 }
 
+// ---- frame-invariant part of the spectral op: per-bin LDS table ---------
+// A thread owns the same bins of one column for every frame of a launch, so
+// what depends only on (fx, fy) is evaluated once per launch into LDS (N/2+1
+// entries: every mask is symmetric in fy) instead of once per bin and frame.
+//   MM_K2_PYR_TAB (pyramid): (m_a, m_b) = the <= 2 middle-band masks that are
+//     nonzero at the bin, in band order (host checks no 3 bands overlap);
+//   MM_MODE_STANDARD: (w, 0), w = calculate_bandpass_weight (:74-122).
+// Levels 0 and L-1 (high/low-pass, always passed) stay inline: ~20 VALU.
+constexpr int MM_K2_PYR_TAB = 2;
+
 template <int LOG2N, int MODE>
-__global__ __launch_bounds__(wg_threads<LOG2N>())
+__device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
+{
+    constexpr int N = 1 << LOG2N;
+    const float ux = (float)fx * (1.0f / (float)N);
+    const float uy = (float)fyy * (1.0f / (float)N);
+    const float fr = __builtin_amdgcn_sqrtf(ux * ux + uy * uy);
+    if constexpr (MODE == MM_MODE_STANDARD) {
+        const float sf = fminf(fr / 0.707f, 1.0f);
+        float w = 1.0f;
+        if (sp.bp_apply) {
+            if (sf < sp.bp_low) w *= __powf(sf * sp.bp_inv_low, sp.bp_steep);
+            if (sf > sp.bp_high) w *= __powf((1.0f - sf) * sp.bp_inv_1mhigh, sp.bp_steep);
+            w *= sp.bp_sens;
+            if (sf > sp.bp_low && sf < sp.bp_high)
+                w *= 1.0f + sp.bp_edge * __sinf(kPi * (sf - sp.bp_low) * sp.bp_inv_band);
+            w = fmaxf(w, 0.0f);
+        }
+        return make_float2(w, 0.0f);
+    } else {
+        float ma = 0.0f, mb = 0.0f;
+        for (int i = 1; i < sp.L - 1; ++i) {
+            if (fr >= sp.lo[i] && fr <= sp.hi[i]) {
+                const float m = 0.5f * (1.0f + __cosf(2.0f * kPi * ((fr - sp.lo[i]) * sp.inv_w[i] - 0.5f)));
+                if (m != 0.0f) {
+                    if (ma == 0.0f) ma = m;
+                    else mb = m;
+                }
+            }
+        }
+        return make_float2(ma, mb);
+    }
+}
+
+// pyramid_op with the middle bands from the table (same arithmetic, same order)
+template <int LOG2N>
+__device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spec &sp, float2 mt)
+{
+    constexpr int N = 1 << LOG2N;
+    const float ux = (float)fx * (1.0f / (float)N);
+    const float uy = (float)(fy <= N / 2 ? fy : N - fy) * (1.0f / (float)N);
+    const float fr = __builtin_amdgcn_sqrtf(ux * ux + uy * uy);
+    const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
+    float mpass = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
+    if (sp.L > 1)
+        mpass += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+    float mmag = 0.0f;
+    if (mt.x * mt.x * mn2 < sp.tau2) mpass += mt.x;
+    else mmag += mt.x;
+    if (mt.y * mt.y * mn2 < sp.tau2) mpass += mt.y;
+    else mmag += mt.y;
+    c2 a = scale(c, mpass * sp.inv_nn);
+    if (mmag > 0.0f) {
+        const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
+        const float ph = sp.S * d;
+        const float k = mmag * sp.inv_nn;
+        a = add(a, scale(mul(c, mk(__cosf(ph), __sinf(ph))), k));
+    }
+    return a;
+}
+
+template <int MODE>
+__device__ __forceinline__ c2 standard_op_t(c2 c, c2 p, const Spec &sp, float2 mt)
+{
+    const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
+    if (mn2 < sp.tau2) return scale(c, sp.inv_nn);
+    const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
+    const float ph = (d * mt.x) * sp.S;
+    return scale(mul(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
+}
+
+// MODE: MM_MODE_PYRAMID (dynamic masks), MM_MODE_STANDARD or MM_K2_PYR_TAB (tables)
+template <int LOG2N, int MODE>
+__device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, const float2 *tab)
+{
+    constexpr int N = 1 << LOG2N;
+    if constexpr (MODE == MM_MODE_PYRAMID) {
+        return pyramid_op<LOG2N>(c, p, fx, fy, sp);
+    } else {
+        const float2 mt = tab[fy <= N / 2 ? fy : N - fy];
+        if constexpr (MODE == MM_MODE_STANDARD) return standard_op_t<MODE>(c, p, sp, mt);
+        else return pyramid_op_t<LOG2N>(c, p, fx, fy, sp, mt);
+    }
+}
+
+template <int LOG2N> constexpr int k2_tab_entries() { return (1 << LOG2N) / 2 + 1; }
+// dynamic LDS of k_cols: per group the FFT exchange buffer and two tables
+template <int LOG2N> constexpr size_t k2_lds_bytes()
+{
+    return (size_t)groups_per_wg<LOG2N>() *
+           (sizeof(c2) * lds_complex<(1 << LOG2N)>() + 2 * sizeof(float2) * k2_tab_entries<LOG2N>());
+}
+
+// Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
+// f = N/2 (row DFT bins that are real for real rows, so their column spectra are
+// Hermitian in fy) share group 0 of block 0 as one complex column z = G0 + i*GN:
+// the op runs on fy <= N/2 for both and the upper half is mirrored, through the
+// exchange buffer: the upper half of Z is stored for the partner reads
+// Z[N - fy], and the mirrored A goes into the (unused) lower half.  The
+// grid is then exactly N/2 groups (1024 at N=2048: one resident round at 4
+// WGs/CU instead of 1025 with a one-WG tail).  Column N/2's F_{t-1} lives in the
+// state buffer between frames.
+template <int LOG2N, int MODE>
+__global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_t q_stride,
             const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
             Geo g, Spec sp, const c2 *__restrict__ tw)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int TE = k2_tab_entries<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     const int grp = threadIdx.x / T, t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
+    float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * 2 * TE;
+    float2 *tabN = tab0 + TE;
     const int f_raw = blockIdx.x * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
     const bool blk0 = blockIdx.x == 0;        // uniform: block 0 runs the extra exchanges
     const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
     c2 *stN = state_out + (size_t)(N / 2) * N;
+
+    if constexpr (MODE != MM_MODE_PYRAMID) {
+        for (int e = t0; e < TE; e += T) {
+            tab0[e] = bin_static<LOG2N, MODE>(f, e, sp);
+            if (packed) tabN[e] = bin_static<LOG2N, MODE>(N / 2, e, sp);
+        }
+        __syncthreads();
+    }
 
     c2 prev[8];
 #pragma unroll
@@ -366,62 +482,62 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
         fft_regs<LOG2N, -1>(v, t, lds, tw);
         const bool pass_frame = fr == 0 && first_passthrough;
         if (blk0) {
+            // packed group: Z = F0 + i FN.  Upper half of Z to LDS for the partner
+            // reads (bins fy <= N/2 live in j < 4, plus fy = N/2 at t = 0, j = 4).
+            if (packed) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) lds[pad8(t + j * T)] = v[j];
-            __syncthreads();
-        }
-        if (packed) {
-            // unpack Z = F0 + i FN:  F0 = (Z + conj Zm)/2, FN = (Z - conj Zm)/2i, Zm = Z[N-fy]
-            c2 *A0 = lds + lds_complex<N>(), *AN = A0 + (N / 2 + 1);
-            const c2 *pNsrc = fr ? stN : (state_in ? state_in + (size_t)(N / 2) * N : nullptr);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                __builtin_amdgcn_sched_barrier(0);
-                const int fy = t + j * T;
-                const c2 z = lds[pad8(fy)], zm = lds[pad8((N - fy) & (N - 1))];
-                const c2 f0 = mk(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-                const c2 fN = mk(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
-                if (!pass_frame && fy <= N / 2) {
-                    const c2 pn = pNsrc ? pNsrc[fy] : mk(0.0f, 0.0f);
-                    A0[fy] = spectral_op<LOG2N, MODE>(f0, prev[j], 0, fy, sp);
-                    AN[fy] = spectral_op<LOG2N, MODE>(fN, pn, N / 2, fy, sp);
-                }
-                prev[j] = f0;
-                stN[fy] = fN;
+                for (int j = 4; j < 8; ++j) lds[pad8(t + j * T)] = v[j];
             }
-            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+            if (packed) {
+                const c2 *pNsrc = fr ? stN : (state_in ? state_in + (size_t)(N / 2) * N : nullptr);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int fy = t + j * T;
+                    if (j < 4 || fy == N / 2) {
+                        // partner Z[N - fy]: upper half (fy = 0, N/2 pair with themselves)
+                        const c2 z = v[j];
+                        const c2 zm = (fy == 0 || fy == N / 2) ? z : lds[pad8(N - fy)];
+                        const c2 f0 = mk(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+                        const c2 fN = mk(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+                        if (!pass_frame) {
+                            const c2 pn = pNsrc ? pNsrc[fy] : mk(0.0f, 0.0f);
+                            const c2 a0 = k2_op<LOG2N, MODE>(f0, prev[j], 0, fy, sp, tab0);
+                            const c2 an = k2_op<LOG2N, MODE>(fN, pn, N / 2, fy, sp, tabN);
+                            v[j] = mk(a0.x - an.y, a0.y + an.x);   // A0 + i AN
+                            if (j < 4)   // bin N - fy reads conj(A0) + i conj(AN)
+                                lds[pad8(fy)] = mk(a0.x + an.y, an.x - a0.y);
+                        }
+                        prev[j] = f0;
+                        stN[fy] = fN;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+            if (packed && !pass_frame) {
+#pragma unroll
+                for (int j = 4; j < 8; ++j) {
+                    const int fy = t + j * T;
+                    if (fy != N / 2) v[j] = lds[pad8(N - fy)];
+                }
+            }
+            __syncthreads();   // the inverse FFT rewrites the buffer
         }
         if (pass_frame) {
             if (!packed) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) prev[j] = v[j];
             }
-            if (blk0) __syncthreads();
             continue;
-        }
-        if (blk0) {
-            __syncthreads();
-            if (packed) {
-                const c2 *A0 = lds + lds_complex<N>(), *AN = A0 + (N / 2 + 1);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int fy = t + j * T;
-                    const int src = fy <= N / 2 ? fy : N - fy;   // Hermitian: A[fy] = conj A[N-fy]
-                    c2 a0 = A0[src], an = AN[src];
-                    if (fy > N / 2) {
-                        a0.y = -a0.y;
-                        an.y = -an.y;
-                    }
-                    v[j] = mk(a0.x - an.y, a0.y + an.x);   // A0 + i AN
-                }
-            }
         }
         if (!packed) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 // one bin at a time: keeps the 8 op instances from being interleaved
                 __builtin_amdgcn_sched_barrier(0);
-                const c2 a = spectral_op<LOG2N, MODE>(v[j], prev[j], f, t + j * T, sp);
+                const c2 a = k2_op<LOG2N, MODE>(v[j], prev[j], f, t + j * T, sp, tab0);
                 prev[j] = v[j];
                 v[j] = a;
             }
@@ -446,8 +562,27 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
         }
     }
     if (valid) {
+        if (packed) {
+            // column 0: bins fy <= N/2 in prev[0..4]; the rest is the Hermitian
+            // mirror (bitwise: F0[N-fy] = conj F0[fy] by the unpack formula).
+            // Column N/2 (stN) is mirrored the same way (rows fy <= N/2 were
+            // written by this same thread in the frame loop).
 #pragma unroll
-        for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t0 + j * T] = prev[j];
+            for (int j = 0; j < 5; ++j) {
+                const int fy = t0 + j * T;
+                if (j < 4 || fy == N / 2) {
+                    state_out[fy] = prev[j];
+                    if (fy != 0 && fy != N / 2) {
+                        state_out[N - fy] = mk(prev[j].x, -prev[j].y);
+                        const c2 n = stN[fy];
+                        stN[N - fy] = mk(n.x, -n.y);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t0 + j * T] = prev[j];
+        }
     }
 }
 

@@ -80,7 +80,7 @@ __device__ __forceinline__ c2 rot16(c2 a)
     constexpr float si = EXP == 1 ? S : EXP == 2 ? H : EXP == 3 ? C : EXP == 4 ? 1.0f
                        : EXP == 6 ? H : -S;
     if constexpr (EXP == 4) return mul_i<DIR>(a);
-    else return mk(a.x * cr - a.y * (DIR * si), a.x * (DIR * si) + a.y * cr);
+    else return mul_p(a, c2{cr, DIR * si}, c2{-DIR * si, cr});
 }
 
 // 16-point DFT, natural order in and out: 4 x DFT4, twiddles W16^(n2 k1), 4 x DFT4.
@@ -118,37 +118,6 @@ __device__ __forceinline__ void dft(c2 *u)
     else if constexpr (R == 8) dft8<DIR>(u);
     else if constexpr (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
     else dft2<DIR>(u[0], u[1]);
-}
-
-// u[t] *= w^t, w^t by products of the base (<= 4 roundings for t < 16)
-template <int R>
-__device__ __forceinline__ void apply_twiddles(c2 *u, c2 w1)
-{
-    if constexpr (R >= 2) u[1] = mul(u[1], w1);
-    if constexpr (R >= 4) {
-        const c2 w2 = mul(w1, w1), w3 = mul(w2, w1);
-        u[2] = mul(u[2], w2);
-        u[3] = mul(u[3], w3);
-        if constexpr (R >= 8) {
-            const c2 w4 = mul(w2, w2);
-            u[4] = mul(u[4], w4);
-            u[5] = mul(u[5], mul(w4, w1));
-            u[6] = mul(u[6], mul(w4, w2));
-            u[7] = mul(u[7], mul(w4, w3));
-            if constexpr (R >= 16) {
-                const c2 w8 = mul(w4, w4);
-                u[8] = mul(u[8], w8);
-                u[9] = mul(u[9], mul(w8, w1));
-                u[10] = mul(u[10], mul(w8, w2));
-                u[11] = mul(u[11], mul(w8, w3));
-                const c2 w12 = mul(w8, w4);
-                u[12] = mul(u[12], w12);
-                u[13] = mul(u[13], mul(w12, w1));
-                u[14] = mul(u[14], mul(w12, w2));
-                u[15] = mul(u[15], mul(w12, w3));
-            }
-        }
-    }
 }
 
 // Twiddle bases of every pass, issued up front (latency hides under pass 0).
