@@ -78,6 +78,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nb)
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// Access at a 32-bit BYTE offset from a (workgroup-uniform) base: matches the
+// scalar-base + 32-bit vector-offset form of global loads/stores (an index
+// scaled as zext(i) * sizeof(T) needs 64-bit address math per access).
+template <class T>
+__device__ __forceinline__ T ld_off(const void *base, unsigned byte_off)
+{
+    return *reinterpret_cast<const T *>(reinterpret_cast<const uint8_t *>(base) + byte_off);
+}
+template <class T>
+__device__ __forceinline__ void st_off(void *base, unsigned byte_off, T v)
+{
+    *reinterpret_cast<T *>(reinterpret_cast<uint8_t *>(base) + byte_off) = v;
+}
+
 // ---- pixel access -------------------------------------------------------
 template <int FMT> struct Pix;
 template <> struct Pix<0> {           // RGBA8 UNORM
@@ -94,11 +108,11 @@ template <> struct Pix<0> {           // RGBA8 UNORM
                            (float)((u >> 16) & 255u) * s, (float)(u >> 24) * s);
     }
     __device__ static float4 load(const uint8_t *base, size_t i) { return cvt(raw(base, i)); }
-    __device__ static void store(uint8_t *base, size_t i, float r, float g, float b)
+    __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
     {
         uint32_t R = (uint32_t)(r * 255.0f + 0.5f), G = (uint32_t)(g * 255.0f + 0.5f),
                  B = (uint32_t)(b * 255.0f + 0.5f);
-        reinterpret_cast<uint32_t *>(base)[i] = R | (G << 8) | (B << 16) | (255u << 24);
+        st_off<uint32_t>(base, i * 4u, R | (G << 8) | (B << 16) | (255u << 24));
     }
 };
 template <> struct Pix<1> {           // RGBA32F
@@ -110,9 +124,9 @@ template <> struct Pix<1> {           // RGBA32F
     }
     __device__ static float4 cvt(raw_t v) { return v; }
     __device__ static float4 load(const uint8_t *base, size_t i) { return raw(base, i); }
-    __device__ static void store(uint8_t *base, size_t i, float r, float g, float b)
+    __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
     {
-        reinterpret_cast<float4 *>(base)[i] = make_float4(r, g, b, 1.0f);
+        st_off<float4>(base, i * 16u, make_float4(r, g, b, 1.0f));
     }
 };
 
@@ -121,6 +135,21 @@ __device__ __forceinline__ float luma(float4 c) { return 0.299f * c.x + 0.587f *
 __device__ __forceinline__ float chroma_i(float4 c) { return 0.596f * c.x + -0.274f * c.y + -0.322f * c.z; }
 __device__ __forceinline__ float chroma_q(float4 c) { return 0.211f * c.x + -0.523f * c.y + 0.312f * c.z; }
 __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
+
+// (I, Q) of a raw pixel.  RGBA8: the 1/255 of the UNORM read is folded into the
+// RGBToYIQ coefficients (3 byte converts + 6 FMAs).
+template <int FMT>
+__device__ __forceinline__ float2 chroma_iq(typename Pix<FMT>::raw_t u)
+{
+    if constexpr (FMT == 0) {
+        constexpr float k = 1.0f / 255.0f;
+        const float r = (float)(u & 255u), gg = (float)((u >> 8) & 255u), b = (float)((u >> 16) & 255u);
+        return make_float2((0.596f * k) * r + (-0.274f * k) * gg + (-0.322f * k) * b,
+                           (0.211f * k) * r + (-0.523f * k) * gg + (0.312f * k) * b);
+    } else {
+        return make_float2(chroma_i(u), chroma_q(u));
+    }
+}
 
 // =========================================================================
 // K1: luma rows -> half spectra of row pairs
@@ -685,36 +714,46 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
     const int i0 = rt * TR, c0 = ct * TC;
     const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
 
-    constexpr int E = (TR + 2) * WC, IT = (E + TC - 1) / TC;
-    typename Pix<FMT>::raw_t px[IT];
+    // Staged entry (sr, j) is source pixel (row i0-1+sr, column c0-1+j), wrapped
+    // or clamped like the resample's sampler.  Rows are workgroup-uniform (scalar
+    // base pointers); thread tid stages column j = tid of every row, and threads
+    // 0, 1 also the halo columns j = TC, TC+1.
+    using raw_t = typename Pix<FMT>::raw_t;
+    // 32-bit offsets from workgroup-uniform row pointers: scalar base + vector
+    // offset addressing, no 64-bit address math per access
+    const unsigned colA = (unsigned)wrap_near(min(c0 - 1 + tid, g.W), g.W, g.edge);
+    raw_t pa[TR + 2];
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {   // all staging loads in flight, then convert
-        const int e = min(tid + it * TC, E - 1);
-        const int sr = e / WC, j = e - sr * WC;
+    for (int sr = 0; sr < TR + 2; ++sr) {   // all staging loads in flight, then convert
         const int row = wrap_near(min(i0 - 1 + sr, g.H), g.H, g.edge);
-        const int col = wrap_near(min(c0 - 1 + j, g.W), g.W, g.edge);
-        px[it] = Pix<FMT>::raw(img, (size_t)row * g.W + col);
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int e = tid + it * TC;
-        const float4 c = Pix<FMT>::cvt(px[it]);
-        if (e < E) iq[e] = make_float2(chroma_i(c), chroma_q(c));
+        pa[sr] = ld_off<raw_t>(img, (unsigned)(row * g.W + colA) * Pix<FMT>::bpp);
     }
     const int X = c0 + tid;
     const bool vx = X < g.W;
+    const float4 wc = colW3[min(X, g.W - 1)];
     // Yh of this column for the TR+4 canvas rows y0+i0-2 .. y0+i0+TR+1 (wrapped
-    // or clamped like the blur's sampler, then mapped to Yh list rows)
+    // or clamped like the blur's sampler, then mapped to Yh list rows), issued
+    // before the I/Q conversions so that all loads share one memory round trip
     const float *Yf = Yh + (size_t)frame * yh_stride;
+    const unsigned Xc = (unsigned)min(X, g.W - 1);
     float yv[TR + 4];
 #pragma unroll
     for (int v = 0; v < TR + 4; ++v) {   // unconditional loads at clamped addresses
         const int cy = wrap_near(g.y0 + i0 - 2 + v, g.N, g.edge);
         const int k = (cy - g.rb + 2 * g.N) & (g.N - 1);
-        const float y = Yf[(size_t)min(k, g.Hn - 1) * g.W + min(X, g.W - 1)];
+        const float y = ld_off<float>(Yf, (unsigned)(min(k, g.Hn - 1) * g.W + Xc) * 4u);
         yv[v] = k < g.Hn ? y : 0.0f;
     }
-    const float4 wc = vx ? colW3[X] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // halo columns j = TC, TC + 1 of the TR + 2 rows: one entry for each of
+    // threads 0 .. 2(TR+2)-1, loaded with the others (unconditional, clamped)
+    constexpr int NH = 2 * (TR + 2);
+    const int hs = min(tid, NH - 1);
+    const int hrow = wrap_near(min(i0 - 1 + (hs >> 1), g.H), g.H, g.edge);
+    const int hcol = wrap_near(min(c0 - 1 + TC + (hs & 1), g.W), g.W, g.edge);
+    const raw_t ph = ld_off<raw_t>(img, (unsigned)(hrow * g.W + hcol) * Pix<FMT>::bpp);
+    if (tid < NH) iq[(hs >> 1) * WC + TC + (hs & 1)] = chroma_iq<FMT>(ph);
+#pragma unroll
+    for (int sr = 0; sr < TR + 2; ++sr) iq[sr * WC + tid] = chroma_iq<FMT>(pa[sr]);
     __syncthreads();
     if (!vx) return;
     float hi[TR + 2], hq[TR + 2];
@@ -738,7 +777,7 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
             const float rr = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
             const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
             const float bb = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
-            Pix<FMT>::store(outp, (size_t)i * g.W + X, rr, gg, bb);
+            Pix<FMT>::store(outp + (unsigned)(i * g.W * Pix<FMT>::bpp), (unsigned)X, rr, gg, bb);
         }
     }
 }
