@@ -488,13 +488,21 @@ static bool taps_local(const std::vector<Tap4> &tab)
     return true;
 }
 
-static std::vector<float4> merge3(const std::vector<Tap4> &tab)
+// Taps merged onto offsets -1, 0, +1; .w carries the wrapped (edge-mode) indices
+// of i-1 and i+1 as bits (i-1) | (i+1) << 16 (k_rows_fwd's horizontal pass).
+static std::vector<float4> merge3(const std::vector<Tap4> &tab, int edge)
 {
+    const int n = (int)tab.size();
     std::vector<float4> out(tab.size());
-    for (size_t i = 0; i < tab.size(); ++i) {
+    for (int i = 0; i < n; ++i) {
         float w[3] = {0.0f, 0.0f, 0.0f};
-        for (int m = 0; m < 4; ++m) w[tab[i].idx[m] - (int)i + 1] += tab[i].w[m];
-        out[i] = make_float4(w[0], w[1], w[2], 0.0f);
+        for (int m = 0; m < 4; ++m) w[tab[i].idx[m] - i + 1] += tab[i].w[m];
+        const int l = i > 0 ? i - 1 : (edge ? 0 : n - 1);
+        const int r = i < n - 1 ? i + 1 : (edge ? n - 1 : 0);
+        const uint32_t bits = (uint32_t)l | ((uint32_t)r << 16);
+        float wb;
+        memcpy(&wb, &bits, sizeof(wb));
+        out[i] = make_float4(w[0], w[1], w[2], wb);
     }
     return out;
 }
@@ -505,7 +513,7 @@ static int upload_tables(mm_handle *h)
     build_tab(h->W, h->N, h->p.edge_mode, col);
     build_tab(h->H, h->N, h->p.edge_mode, row);
     if (!taps_local(col) || !taps_local(row)) return MM_ERR_UNSUPPORTED;  // k_compose tiling
-    const std::vector<float4> c3 = merge3(col), r3 = merge3(row);
+    const std::vector<float4> c3 = merge3(col, h->p.edge_mode), r3 = merge3(row, h->p.edge_mode);
     HIPCHK(hipMemcpy(h->d_col3, c3.data(), sizeof(float4) * h->W, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_row3, r3.data(), sizeof(float4) * h->H, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_col, col.data(), sizeof(Tap4) * h->W, hipMemcpyHostToDevice));

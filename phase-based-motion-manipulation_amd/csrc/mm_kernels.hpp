@@ -136,6 +136,19 @@ __device__ __forceinline__ float chroma_i(float4 c) { return 0.596f * c.x + -0.2
 __device__ __forceinline__ float chroma_q(float4 c) { return 0.211f * c.x + -0.523f * c.y + 0.312f * c.z; }
 __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
 
+// Y of a raw pixel (RGBA8: 1/255 folded into the RGBToYIQ row).
+template <int FMT>
+__device__ __forceinline__ float luma_raw(typename Pix<FMT>::raw_t u)
+{
+    if constexpr (FMT == 0) {
+        constexpr float k = 1.0f / 255.0f;
+        return (0.299f * k) * (float)(u & 255u) + (0.587f * k) * (float)((u >> 8) & 255u) +
+               (0.114f * k) * (float)((u >> 16) & 255u);
+    } else {
+        return luma(u);
+    }
+}
+
 // (I, Q) of a raw pixel.  RGBA8: the 1/255 of the UNORM read is folded into the
 // RGBToYIQ coefficients (3 byte converts + 6 FMAs).
 template <int FMT>
@@ -163,7 +176,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = threadIdx.x / T, t = threadIdx.x % T;
+    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
     const bool valid = logical < total_pairs;
@@ -175,29 +188,33 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     // Taps of image row r lie on source rows r-1..r+1 (w3 tables), so the pair
     // (ra, ra+1) reads the 4 source rows ra-1..ra+2.
     float *V = reinterpret_cast<float *>(lds);
+    using raw_t = typename Pix<FMT>::raw_t;
+    constexpr int BPP = Pix<FMT>::bpp;
+    // RGBA8: all 32 pixel loads of the thread in one batch; RGBA32F (4x the
+    // registers): two batches of 16
+    constexpr int UB = FMT == 0 ? 8 : 4;
     if (valid) {
         const float4 wa = rowW3[ra], wb = rowW3[ra + 1];
-        int sr[4];
+        const uint8_t *rowp[4];   // workgroup-uniform source row pointers
 #pragma unroll
-        for (int d = 0; d < 4; ++d) sr[d] = wrap_near(ra - 1 + d, g.H, g.edge);
-        // W <= N = 8T: at most 8 columns per thread, in two batches of 4 so the
-        // 16 loads of a batch are in flight together
+        for (int d = 0; d < 4; ++d) rowp[d] = img + (unsigned)(wrap_near(ra - 1 + d, g.H, g.edge) * g.W * BPP);
+        // W <= N = 8T: at most 8 columns per thread
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < 8 / UB; ++h) {
             __builtin_amdgcn_sched_barrier(0);
-            typename Pix<FMT>::raw_t px[4][4];
+            raw_t px[UB][4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = min(t + (h * 4 + u) * T, g.W - 1);
+            for (int u = 0; u < UB; ++u) {
+                const unsigned off = (unsigned)min(t + (h * UB + u) * T, g.W - 1) * BPP;
 #pragma unroll
-                for (int d = 0; d < 4; ++d) px[u][d] = Pix<FMT>::raw(img, (size_t)sr[d] * g.W + i);
+                for (int d = 0; d < 4; ++d) px[u][d] = ld_off<raw_t>(rowp[d], off);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = t + (h * 4 + u) * T;
+            for (int u = 0; u < UB; ++u) {
+                const int i = t + (h * UB + u) * T;
                 float l[4];
 #pragma unroll
-                for (int d = 0; d < 4; ++d) l[d] = luma(Pix<FMT>::cvt(px[u][d]));
+                for (int d = 0; d < 4; ++d) l[d] = luma_raw<FMT>(px[u][d]);
                 if (i < g.W) {
                     V[i] = wa.x * l[0] + wa.y * l[1] + wa.z * l[2];
                     V[g.W + i] = wb.x * l[1] + wb.y * l[2] + wb.z * l[3];
@@ -212,8 +229,9 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         if (j == 4) __builtin_amdgcn_sched_barrier(0);     // two batches: bound VGPRs
         const int i = t + j * T - g.x0;                    // image column
         const int ic = min(max(i, 0), g.W - 1);
-        const float4 w = colW3[ic];                         // source columns i-1, i, i+1
-        const int cl = wrap_near(ic - 1, g.W, g.edge), cr = wrap_near(ic + 1, g.W, g.edge);
+        const float4 w = colW3[ic];   // weights of source columns i-1, i, i+1; .w: wrapped
+        const unsigned nb = __float_as_uint(w.w);          // (i-1) | (i+1) << 16
+        const int cl = nb & 0xffffu, cr = nb >> 16;
         const float ya = w.x * V[cl] + w.y * V[ic] + w.z * V[cr];
         const float yb = w.x * V[g.W + cl] + w.y * V[g.W + ic] + w.z * V[g.W + cr];
         const bool in = valid && i >= 0 && i < g.W;
@@ -234,7 +252,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         o.y = 0.5f * (zf.y - zm.y);
         o.z = 0.5f * (zf.y + zm.y);
         o.w = -0.5f * (zf.x - zm.x);
-        *reinterpret_cast<float4 *>(Gf + (size_t)f * g.H + ra) = o;
+        st_off<float4>(Gf, (unsigned)(f * g.H + ra) * 8u, o);
     };
 #pragma unroll
     for (int j = 0; j < 4; ++j) split_store(t + j * T);
@@ -465,7 +483,7 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
     constexpr int TE = k2_tab_entries<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = threadIdx.x / T, t0 = threadIdx.x % T;
+    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * 2 * TE;
     float2 *tabN = tab0 + TE;
@@ -629,7 +647,7 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = threadIdx.x / T, t = threadIdx.x % T;
+    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
     const bool valid = logical < total_pairs;
