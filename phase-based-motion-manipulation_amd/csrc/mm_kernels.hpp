@@ -366,10 +366,13 @@ __device__ __forceinline__ c2 spectral_op(c2 c, c2 p, int fx, int fy, const Spec
 // A thread owns the same bins of one column for every frame of a launch, so
 // what depends only on (fx, fy) is evaluated once per launch into LDS (N/2+1
 // entries: every mask is symmetric in fy) instead of once per bin and frame.
-//   MM_K2_PYR_TAB (pyramid): (m_a, m_b) = the <= 2 middle-band masks that are
-//     nonzero at the bin, in band order (host checks no 3 bands overlap);
+//   MM_K2_PYR_TAB (pyramid): x = m_a, the first middle-band mask nonzero at
+//     the bin; y = -(hp + lp), the always-passed levels 0 and L-1, when at most
+//     one band is nonzero (sign bit set, -0.0 included), else y = m_b, the
+//     second band, and hp + lp is evaluated inline (a divergent branch that
+//     only waves holding such bins take; none for L <= 5 at default bands).
+//     The host checks that no 3 bands overlap.
 //   MM_MODE_STANDARD: (w, 0), w = calculate_bandpass_weight (:74-122).
-// Levels 0 and L-1 (high/low-pass, always passed) stay inline: ~20 VALU.
 constexpr int MM_K2_PYR_TAB = 2;
 
 template <int LOG2N, int MODE>
@@ -392,6 +395,9 @@ __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
         }
         return make_float2(w, 0.0f);
     } else {
+        float mfix = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
+        if (sp.L > 1)
+            mfix += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
         float ma = 0.0f, mb = 0.0f;
         for (int i = 1; i < sp.L - 1; ++i) {
             if (fr >= sp.lo[i] && fr <= sp.hi[i]) {
@@ -402,7 +408,7 @@ __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
                 }
             }
         }
-        return make_float2(ma, mb);
+        return make_float2(ma, mb != 0.0f ? mb : -mfix);
     }
 }
 
@@ -411,18 +417,25 @@ template <int LOG2N>
 __device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spec &sp, float2 mt)
 {
     constexpr int N = 1 << LOG2N;
-    const float ux = (float)fx * (1.0f / (float)N);
-    const float uy = (float)(fy <= N / 2 ? fy : N - fy) * (1.0f / (float)N);
-    const float fr = __builtin_amdgcn_sqrtf(ux * ux + uy * uy);
     const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
-    float mpass = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
-    if (sp.L > 1)
-        mpass += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+    float mpass, mb;
+    if (__builtin_signbit(mt.y)) {   // static hp + lp from the table
+        mpass = -mt.y;
+        mb = 0.0f;
+    } else {                         // two bands at this bin: hp + lp inline
+        const float ux = (float)fx * (1.0f / (float)N);
+        const float uy = (float)(fy <= N / 2 ? fy : N - fy) * (1.0f / (float)N);
+        const float fr = __builtin_amdgcn_sqrtf(ux * ux + uy * uy);
+        mpass = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
+        if (sp.L > 1)
+            mpass += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+        mb = mt.y;
+    }
     float mmag = 0.0f;
     if (mt.x * mt.x * mn2 < sp.tau2) mpass += mt.x;
     else mmag += mt.x;
-    if (mt.y * mt.y * mn2 < sp.tau2) mpass += mt.y;
-    else mmag += mt.y;
+    if (mb * mb * mn2 < sp.tau2) mpass += mb;
+    else mmag += mb;
     c2 a = scale(c, mpass * sp.inv_nn);
     if (mmag > 0.0f) {
         const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
