@@ -582,7 +582,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
               hipMalloc(&h->d_row, sizeof(Tap4) * height) == hipSuccess &&
               hipMalloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
               hipMalloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
-              hipMalloc(&h->d_tw, sizeof(c2) * N) == hipSuccess &&
+              hipMalloc(&h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
               hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * h->chunk) == hipSuccess &&
               hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * h->chunk) == hipSuccess &&
               hipMalloc(&h->d_Yh, sizeof(float) * h->yh_stride * h->chunk) == hipSuccess &&
@@ -591,13 +591,15 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
         free_handle(h);
         return MM_ERR_OOM;
     }
-    std::vector<c2> tw(N);
+    // W_N^k table (mm_fft.hpp tw_entries_v)
+    const int ntw = tw_entries_v(h->log2n);
+    std::vector<c2> tw(ntw);
     for (int k = 0; k < N; ++k) {
         const double a = -2.0 * M_PI * (double)k / (double)N;
         tw[k].x = (float)cos(a);
         tw[k].y = (float)sin(a);
     }
-    if (hipMemcpy(h->d_tw, tw.data(), sizeof(c2) * N, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(h->d_tw, tw.data(), sizeof(c2) * ntw, hipMemcpyHostToDevice) != hipSuccess) {
         free_handle(h);
         return MM_ERR_HIP;
     }

@@ -144,111 +144,96 @@ __device__ __forceinline__ c2 twiddle(const c2 *__restrict__ tw, int idx)
     return DIR < 0 ? w : mk(w.x, -w.y);
 }
 
-// Base twiddle W_{NS*R}^k of butterfly q of a pass (one table load).
-template <int N, int R, int NS, int DIR>
-__device__ __forceinline__ c2 pass_twiddle(int t, int q, const c2 *__restrict__ tw)
-{
-    constexpr int T = N / 8;
-    constexpr int TWS = N / (NS * R);  // twiddle-table stride for W_{NS*R}
-    return twiddle<DIR>(tw, ((t + q * T) & (NS - 1)) * TWS);
-}
+constexpr int fft_passes_v(int log2n) { return log2n / 3 + (log2n % 3 ? 1 : 0); }
+template <int LOG2N> constexpr int fft_passes() { return fft_passes_v(LOG2N); }
+constexpr int pass_radix_v(int log2n, int p) { return (p < log2n / 3) ? 8 : (log2n % 3 == 2 ? 4 : 2); }
+template <int LOG2N, int P> constexpr int pass_radix() { return pass_radix_v(LOG2N, P); }
+constexpr int pass_ns_v(int log2n, int p) { return p == 0 ? 1 : pass_ns_v(log2n, p - 1) * pass_radix_v(log2n, p - 1); }
 
-template <int N, int R, int NS, int DIR, bool LAST, bool DB>
-__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 *wb)
-{
-    constexpr int T = N / 8;
-    constexpr int B = 8 / R;
-#pragma unroll
-    for (int q = 0; q < B; ++q) {
-        const int b = t + q * T;
-        const int k = b & (NS - 1);
-        c2 u[R];
-#pragma unroll
-        for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
-        if (NS > 1) apply_twiddles<R>(u, wb[q]);   // base preloaded at FFT start
-        if (R == 8) dft8<DIR>(u);
-        else if (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
-        else dft2<DIR>(u[0], u[1]);
-        if (LAST) {
-#pragma unroll
-            for (int m = 0; m < R; ++m) v[q + m * B] = u[m];
-        } else {
-            const int base = (b / NS) * NS * R + k;
-#pragma unroll
-            for (int m = 0; m < R; ++m) lds[pad8(base + m * NS)] = u[m];
-        }
-    }
-    if (!LAST) {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = lds[pad8(t + j * T)];
-        // Double-buffered (DB): the next exchange writes the other buffer, and a
-        // buffer is rewritten only after everyone passed the barrier that follows
-        // its reads -- so no second barrier here.
-        if (!DB) __syncthreads();
-    }
-}
+// Twiddle buffer: the N-entry W_N table (tw_entries_v: kept as a function so
+// the buffer layout has one definition).  A pass-table variant (each
+// butterfly's powers loaded as one row) issued fewer VALU instructions but ran
+// slower: its per-pass load latency sits on the short row kernels' critical
+// path; powers are products of one preloaded base instead.
+constexpr int tw_entries_v(int log2n) { return 1 << log2n; }
 
-template <int LOG2N> constexpr int fft_passes() { return LOG2N / 3 + (LOG2N % 3 ? 1 : 0); }
-template <int LOG2N, int P> constexpr int pass_radix()
-{
-    return (P < LOG2N / 3) ? 8 : (LOG2N % 3 == 2 ? 4 : 2);
-}
-
-// Issue every pass's twiddle loads up front (slot P*4+q) so their latency hides
-// under the first pass instead of stalling each pass.
-template <int LOG2N, int DIR, int P, int NS>
+// Base twiddle W_{Ns R}^r of butterfly q of pass P (one table load), for every
+// pass, issued at FFT start so the latency hides under pass 0: slot P*4 + q.
+template <int LOG2N, int DIR, int P = 1>
 __device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
 {
     if constexpr (P < fft_passes<LOG2N>()) {
-        constexpr int R = pass_radix<LOG2N, P>();
-        if constexpr (NS > 1) {
+        constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
+        constexpr int NS = pass_ns_v(LOG2N, P), TWS = N / (NS * R);
 #pragma unroll
-            for (int q = 0; q < 8 / R; ++q) wb[P * 4 + q] = pass_twiddle<(1 << LOG2N), R, NS, DIR>(t, q, tw);
-        }
-        preload_twiddles<LOG2N, DIR, P + 1, NS * R>(wb, t, tw);
+        for (int q = 0; q < B; ++q) wb[P * 4 + q] = twiddle<DIR>(tw, ((t + q * T) & (NS - 1)) * TWS);
+        preload_twiddles<LOG2N, DIR, P + 1>(wb, t, tw);
     }
 }
 
-template <int LOG2N, int DIR, int P, int NS, bool DB>
-__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds0, c2 *lds1,
-                                              const c2 (&wb)[16])
+// One Stockham pass (radix R, stride Ns).  B = 8/R butterflies per thread;
+// butterfly b = t + q*T reads x[b + m*N/R] (= register q + m*B) and writes
+// y[(b/Ns)*Ns*R + b%Ns + m*Ns].
+template <int LOG2N, int P, int DIR>
+__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+{
+    constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
+    constexpr int NS = pass_ns_v(LOG2N, P);
+    constexpr bool LAST = P == fft_passes<LOG2N>() - 1;
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+        const int b = t + q * T;
+        c2 u[R];
+#pragma unroll
+        for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
+        if constexpr (NS > 1) apply_twiddles<R>(u, wb[P * 4 + q]);
+        if constexpr (R == 8) dft8<DIR>(u);
+        else if constexpr (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
+        else dft2<DIR>(u[0], u[1]);
+        if constexpr (LAST) {
+#pragma unroll
+            for (int m = 0; m < R; ++m) v[q + m * B] = u[m];
+        } else {
+            // pad8(base + m Ns) = pad8(base) + m (Ns + Ns/8) for Ns >= 8, and
+            // pad8(base) + m for Ns = 1 (base = 8b): immediate LDS offsets
+            constexpr int step = NS == 1 ? 1 : NS + NS / 8;
+            c2 *row = lds + pad8((b / NS) * NS * R + (b & (NS - 1)));
+#pragma unroll
+            for (int m = 0; m < R; ++m) row[m * step] = u[m];
+        }
+    }
+    if constexpr (!LAST) {
+        __syncthreads();
+        if constexpr (T % 8 == 0) {   // pad8(t + j T) = pad8(t) + j (T + T/8)
+            const c2 *col = lds + pad8(t);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = col[j * (T + T / 8)];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = lds[pad8(t + j * T)];
+        }
+        __syncthreads();
+    }
+}
+
+template <int LOG2N, int DIR, int P>
+__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
 {
     if constexpr (P < fft_passes<LOG2N>()) {
-        constexpr int R = pass_radix<LOG2N, P>();
-        c2 *lds = (DB && (P & 1)) ? lds1 : lds0;
-        fft_pass<(1 << LOG2N), R, NS, DIR, P == fft_passes<LOG2N>() - 1, DB>(v, t, lds, wb + P * 4);
-        fft_pass_loop<LOG2N, DIR, P + 1, NS * R, DB>(v, t, lds0, lds1, wb);
+        fft_pass<LOG2N, P, DIR>(v, t, lds, wb);
+        fft_pass_loop<LOG2N, DIR, P + 1>(v, t, lds, wb);
     }
 }
-
-// LDS exchanges of one FFT; with double buffering, exchange e uses buffer e & 1
-// (relative to the buffers passed in) and the LAST one leaves its buffer
-// "dirty" (slower threads may still read it until the caller's next barrier).
-template <int LOG2N> constexpr int fft_exchanges() { return fft_passes<LOG2N>() - 1; }
-template <int LOG2N> constexpr int fft_dirty_buffer() { return (fft_exchanges<LOG2N>() - 1) & 1; }
 
 // Unnormalised DFT of the group's sequence, DIR=-1 forward, DIR=+1 inverse.
 // Every thread of the WORKGROUP must call this (it contains __syncthreads).
-// Single-buffered form: ends with a barrier, LDS free on return.
+// Ends with a barrier, LDS free on return.  tw: twiddle buffer (tw_entries_v).
 template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
 {
     c2 wb[16];
-    preload_twiddles<LOG2N, DIR, 0, 1>(wb, t, tw);
-    fft_pass_loop<LOG2N, DIR, 0, 1, false>(v, t, lds, lds, wb);
-}
-
-// Double-buffered form over (b0, b1): one barrier per exchange.  On return the
-// buffer fft_dirty_buffer() (0 -> b0, 1 -> b1) may still be read by other
-// threads; the other one is free.
-template <int LOG2N, int DIR>
-__device__ __forceinline__ void fft_regs_db(c2 (&v)[8], int t, c2 *b0, c2 *b1,
-                                            const c2 *__restrict__ tw)
-{
-    c2 wb[16];
-    preload_twiddles<LOG2N, DIR, 0, 1>(wb, t, tw);
-    fft_pass_loop<LOG2N, DIR, 0, 1, true>(v, t, b0, b1, wb);
+    preload_twiddles<LOG2N, DIR>(wb, t, tw);
+    fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wb);
 }
 
 }  // namespace mm

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""VALU issue utilisation per kernel from rocprofv3 PMC + kernel-trace runs.
+
+usage: valu_summary.py PMC_DIR KERNEL_TRACE_DIR OUT_JSON
+
+valu_busy = SQ_INSTS_VALU * 4 cycles / (SIMDs * kernel cycles), with the
+kernel's cycles from its average kernel-trace duration and the shader clock
+derived from SQ_BUSY_CYCLES (summed over the shader engines) over that
+duration.  4 cycles = issue cost of one wave64 VALU instruction on a 16-lane
+SIMD (MI355X_MICROARCH.md, vector-instruction issue table).
+"""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+SIMDS = 256 * 4
+SES = 32        # shader engines summed by SQ_BUSY_CYCLES (8 XCDs x 4)
+
+
+def short(name):
+    m = re.search(r"mm::(k_[a-z_]+)", name)
+    return m.group(1) if m else None
+
+
+pmc = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = short(r["Kernel_Name"])
+        if k:
+            pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+dur = defaultdict(list)
+for f in glob.glob(sys.argv[2] + "/**/*kernel_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = short(r["Kernel_Name"])
+        if k:
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+out = {}
+for k, c in pmc.items():
+    if k not in dur or "SQ_INSTS_VALU" not in c:
+        continue
+    # launches differ in size (chunks); use the largest-launch averages
+    valu = max(c["SQ_INSTS_VALU"])
+    busy = max(c.get("SQ_BUSY_CYCLES", [0]))
+    t = max(dur[k])
+    clk = busy / SES / t if busy else 2.0e9
+    out[k] = {"valu_insts_per_launch": valu, "salu_insts_per_launch": max(c.get("SQ_INSTS_SALU", [0])),
+              "lds_insts_per_launch": max(c.get("SQ_INSTS_LDS", [0])),
+              "launch_s": t, "clock_GHz": round(clk / 1e9, 3),
+              "valu_busy": round(valu * 4 / (SIMDS * clk * t), 3)}
+json.dump(out, open(sys.argv[3], "w"), indent=1)
+for k, v in sorted(out.items()):
+    print(k, v)
