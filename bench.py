@@ -255,6 +255,16 @@ def main():
             traffic = round(per_frame * dk["frames"] / dk["launches"])
         except Exception:
             traffic = None
+    valu = None
+    vfile = os.path.join(ROOT, "profiles", "valu.json")
+    if os.path.exists(vfile):
+        try:
+            vj = json.load(open(vfile))[dom]
+            valu = {"valu_busy": vj["valu_busy"], "valu_insts_per_launch": vj["valu_insts_per_launch"],
+                    "source": "profiles/valu.json (rocprofv3 SQ_INSTS_VALU x 4 cycles / "
+                              "(1024 SIMDs x kernel cycles)); the FFT kernels are VALU-issue-bound"}
+        except Exception:
+            valu = None
     B = survey_bytes_per_frame(W, H, N)
 
     result = {
@@ -273,7 +283,8 @@ def main():
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
                      "bytes_model": "compulsory bytes of the dominant kernel (DESIGN.md §5); "
-                                    "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch"},
+                                    "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch",
+                     "compute": valu},
         "survey_model": {"bytes_per_frame": B,
                          "achieved_GBps_per_gpu": round(B * fps / world / 1e9, 1),
                          "frac": round(B * fps / world / 1e9 / HBM_PEAK_GBPS, 4),
