@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 2
+#define MM_ABI_VERSION 3
 
 /* error codes */
 #define MM_OK               0
@@ -78,6 +78,12 @@ typedef struct {
     float motion_sensitivity;     /* motionSensitivity    .cs:41 */
     int   enhance_edges;          /* enhanceEdges         .cs:42 */
     float edge_enhancement;       /* edgeEnhancement      .cs:43 (used iff enhance_edges, .cs:504) */
+    /* debug views (ProcessDebugView .cs:234-257): while either is set the output
+     * is the |spectrum| (log-scaled) and/or |phase| view, R channel only (RFloat
+     * textures), cropped (one view) or split screen (both); the state still
+     * follows the input (.cs:122).  Since ABI 3. */
+    int   show_magnitude;         /* showMagnitude        .cs:13 */
+    int   show_phase;             /* showPhase            .cs:14 */
 } mm_params;
 
 /* Reference defaults (.cs:12-43): levels 5, 0.05/0.45, phaseScale 10, threshold
@@ -98,8 +104,11 @@ int mm_padded_size(const mm_handle *h, int *n);
 
 /* OnRenderImage (.cs:101-143): one frame in, one frame out.
  * flags & MM_FRAMES_ON_DEVICE: in/out are device pointers and the call is
- * asynchronous on `hip_stream` (NULL = the handle's stream); otherwise in/out
- * are host pointers and the call returns when out is written. */
+ * asynchronous on `hip_stream` (NULL = the default stream, as everywhere in
+ * HIP; mm_stream(h) is a non-blocking stream owned by the handle); otherwise
+ * in/out are host pointers and the call returns when out is written.
+ * Every device-pointer entry point below orders its work on `hip_stream` the
+ * same way: a caller that produced the input on another stream synchronises. */
 int mm_process(mm_handle *h, const void *in, void *out, int format, int flags,
                void *hip_stream);
 
@@ -114,7 +123,7 @@ int mm_reset(mm_handle *h);
 
 /* The temporal state carried between frames: the previous frame's spectrum
  * (what previousSourceTexture, .cs:142, is used for).  `dev_buf` is device
- * memory of mm_state_size() bytes.  Ordered on hip_stream (NULL = handle's). */
+ * memory of mm_state_size() bytes.  Ordered on hip_stream (NULL = default stream). */
 int mm_state_size(const mm_handle *h, size_t *bytes);
 int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream);
 int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stream);

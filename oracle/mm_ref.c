@@ -47,6 +47,8 @@ struct mm_ref {
     /* standard (non-pyramid) mode, .cs:33-43 */
     int standard, bp_apply;
     float bp_low, bp_high, bp_steep, bp_sens, bp_edge;
+    /* debug views showMagnitude / showPhase, .cs:13-14 */
+    int show_mag, show_phase;
 };
 
 /* ------------------------------------------------------------------ */
@@ -229,6 +231,33 @@ void mm_ref_fft_centered(int n, const float *y, float *out_cplx)
         }
     cplx *res = fft2d_passes(n, b1, b2);
     memcpy(out_cplx, res, sizeof(cplx) * nn);
+    free(b1);
+    free(b2);
+}
+
+/* complexBuffer1 after PerformFFT (.cs:508-553), the buffer ProcessDebugView
+ * reads (.cs:243-255).  The ping-pong of .cs:517-549 always ends with the
+ * spectrum in complexBuffer2, so complexBuffer1 holds the state after the
+ * PENULTIMATE column butterfly stage: rows [0,N/2) the N/2-point column DFTs of
+ * the even (centred) rows, rows [N/2,N) those of the odd rows, each row already
+ * fully transformed.  Restated literally (fft2d_passes' b1). */
+void mm_ref_fft_buffer1(int n, const float *y, float *out_cplx)
+{
+    size_t nn = (size_t)n * n;
+    cplx *b1 = (cplx *)malloc(sizeof(cplx) * nn);
+    cplx *b2 = (cplx *)malloc(sizeof(cplx) * nn);
+    #pragma omp parallel for schedule(static)
+    for (int yy = 0; yy < n; ++yy)
+        for (int x = 0; x < n; ++x) {
+            size_t p = (size_t)yy * n + x;
+            float v = y[p];
+            b1[p].x = v; b1[p].y = 0.0f;
+            if (((x + yy) & 1) != 0) { b2[p].x = -b1[p].x; b2[p].y = -b1[p].y; }
+            else b2[p] = b1[p];
+        }
+    cplx *res = fft2d_passes(n, b1, b2);
+    (void)res;   /* == b2 for every n (even + odd stage counts), see above */
+    memcpy(out_cplx, b1, sizeof(cplx) * nn);
     free(b1);
     free(b2);
 }
@@ -522,6 +551,57 @@ void mm_ref_set_state(mm_ref *c, const void *buf)
     memcpy(c->prev, (const char *)buf + 16, sizeof(float) * (size_t)c->W * c->H * 4);
 }
 
+void mm_ref_set_debug(mm_ref *c, int show_magnitude, int show_phase)
+{
+    c->show_mag = show_magnitude ? 1 : 0;
+    c->show_phase = show_phase ? 1 : 0;
+}
+
+/* ConvertComplexMagToTexScaled (FFT.compute:152-161): log10(|z| 10 + 1) / 4 */
+static float debug_mag(cplx z) { return log10f(sqrtf(z.x * z.x + z.y * z.y) * 10.0f + 1.0f) / 4.0f; }
+/* ConvertComplexPhaseToTex (FFT.compute:164-172): |atan2| / PI_2, PI_2 = 1.57079632679 */
+static float debug_phase(cplx z) { return fabsf(atan2f(z.y, z.x)) / 1.57079632679f; }
+
+/* ProcessDebugView (.cs:234-257).  The view textures are RFloat (.cs:321-322):
+ * DstTex.rgb writes keep R only and sampling them yields (v, 0, 0, 1).  One
+ * view: CropTexture (.cs:386-410, texel-exact).  Both: ShowSplitScreen
+ * (.cs:458-487), each N x N texture drawn bilinearly into one half. */
+static void debug_view(mm_ref *c, const float *in, float *out)
+{
+    const int W = c->W, H = c->H, N = c->N;
+    const size_t nn = (size_t)N * N;
+    float *pad = (float *)malloc(sizeof(float) * nn * 4);
+    float *ybuf = (float *)malloc(sizeof(float) * nn);
+    cplx *B = (cplx *)malloc(sizeof(cplx) * nn);
+    float *mag = (float *)malloc(sizeof(float) * nn);
+    float *pha = (float *)malloc(sizeof(float) * nn);
+    mm_ref_pad_window(c, in, pad);                            /* :236-237 */
+    for (size_t p = 0; p < nn; ++p) ybuf[p] = pad[p * 4];     /* :238 */
+    mm_ref_fft_buffer1(N, ybuf, (float *)B);                  /* :239 */
+    #pragma omp parallel for schedule(static)
+    for (long p = 0; p < (long)nn; ++p) {
+        mag[p] = debug_mag(B[p]);
+        pha[p] = debug_phase(B[p]);
+    }
+    const int x0 = (N - W) / 2, y0 = (N - H) / 2;
+    #pragma omp parallel for schedule(static)
+    for (int Y = 0; Y < H; ++Y)
+        for (int X = 0; X < W; ++X) {
+            float v;
+            if (c->show_mag && c->show_phase) {
+                const int right = 2 * X + 1 >= W;
+                const float u = (float)(2 * X + 1 - (right ? W : 0)) / (float)W;
+                const float vv = (float)(2 * Y + 1) / (float)(2 * H);
+                sample_bilinear(right ? pha : mag, N, N, 1, u, vv, c->edge_mode, &v);
+            } else {
+                v = (c->show_mag ? mag : pha)[(size_t)(y0 + Y) * N + x0 + X];
+            }
+            float *o = out + ((size_t)Y * W + X) * 4;
+            o[0] = v; o[1] = 0.0f; o[2] = 0.0f; o[3] = 1.0f;
+        }
+    free(pad); free(ybuf); free(B); free(mag); free(pha);
+}
+
 /* ProcessFrameWithPyramidDecomposition (.cs:145-206); with c->standard the
  * spectral step is ProcessFrameWithStandardMagnification's (.cs:208-232) */
 static void process_pyramid(mm_ref *c, const float *in, float *out, mm_ref_dbg *dbg)
@@ -646,6 +726,11 @@ void mm_ref_process(mm_ref *c, const float *in, float *out, mm_ref_dbg *dbg)
         c->first = 0;
         return;
     }
+    if (c->show_mag || c->show_phase) {                    /* :119-123 */
+        debug_view(c, in, out);
+        memcpy(c->prev, in, sizeof(float) * px);
+        return;
+    }
     if (c->apply) process_pyramid(c, in, out, dbg);        /* :126-136 (both modes) */
     else memcpy(out, in, sizeof(float) * px);              /* :139 */
     memcpy(c->prev, in, sizeof(float) * px);               /* :142 */
@@ -656,7 +741,7 @@ void mm_ref_process_u8(mm_ref *c, const uint8_t *in, uint8_t *out)
     const size_t px = (size_t)c->W * c->H * 4;
     float *fi = (float *)malloc(sizeof(float) * px);
     float *fo = (float *)malloc(sizeof(float) * px);
-    int passthrough = c->first || !c->apply;
+    int passthrough = c->first || (!c->apply && !c->show_mag && !c->show_phase);
     for (size_t i = 0; i < px; ++i) fi[i] = (float)in[i] / 255.0f;
     mm_ref_process(c, fi, fo, NULL);
     if (passthrough) memcpy(out, in, px);                  /* bitwise copy */

@@ -73,9 +73,17 @@ void    mm_ref_process(mm_ref *ctx, const float *in_rgba, float *out_rgba,
 /* Same on RGBA8 frames: in = u8/255 (UNORM), out = round(saturate(v)*255). */
 void    mm_ref_process_u8(mm_ref *ctx, const uint8_t *in_rgba, uint8_t *out_rgba);
 
+/* showMagnitude / showPhase (.cs:13-14): ProcessDebugView (.cs:234-257)
+ * replaces the magnified output while either is set (state still follows
+ * the input, .cs:122).                                                      */
+void    mm_ref_set_debug(mm_ref *ctx, int show_magnitude, int show_phase);
+
 /* ---- stage-level entry points for known-answer tests ---- */
 /* PerformFFT (.cs:508-553): centered forward 2D FFT of a real N*N image.   */
 void    mm_ref_fft_centered(int n, const float *y, float *out_cplx);
+/* complexBuffer1 after PerformFFT: what ProcessDebugView reads (.cs:239-255);
+ * the state after the penultimate column stage (see mm_ref.c).              */
+void    mm_ref_fft_buffer1(int n, const float *y, float *out_cplx);
 /* PerformIFFT (.cs:563-620): |ifft| of a centered N*N spectrum.            */
 void    mm_ref_ifft_mag(int n, const float *in_cplx, float *out_mag);
 /* GeneratePyramidFilters (PyramidOperations.compute:25-87) for one level.   */

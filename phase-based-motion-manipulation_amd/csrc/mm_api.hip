@@ -44,6 +44,8 @@ struct mm_handle {
     Tap4 *d_col, *d_row;
     float4 *d_col3, *d_row3;    // the same taps merged onto offsets -1, 0, +1
     c2 *d_tw;
+    c2 *d_tw_half;              // W_{N/2} table (debug views, lazily)
+    float *d_dbg;               // debug view textures [chunk][mag, phase][N][N] (lazily)
     c2 *d_G, *d_Q, *d_state;
     float *d_Yh;
     size_t g_stride, q_stride, yh_stride;  // elements per frame
@@ -317,6 +319,53 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
 }
 
 // One batch of `n` consecutive frames (n <= chunk), all on the device.
+// ProcessDebugView (.cs:119-123, :234-257) for chunk frames [first, n): K1's half
+// spectra -> k_dbg_cols (view textures) -> k_dbg_out (crop or split screen);
+// the state then follows the last input frame (.cs:122).
+template <int LOG2N>
+static int run_debug(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int first, int fmt,
+                     hipStream_t s)
+{
+    constexpr int N = 1 << LOG2N;
+    int rc;
+    if (n > first) {
+        const size_t tex_stride = (size_t)2 * N * N;
+        if (!h->d_dbg) {   // lazily: only handles that show a debug view pay for it
+            HIPCHK(hipMalloc(&h->d_dbg, sizeof(float) * tex_stride * h->chunk));
+            std::vector<c2> twh(N / 2);
+            for (int k = 0; k < N / 2; ++k) {
+                const double a = -2.0 * M_PI * (double)k / (double)(N / 2);
+                twh[k] = mk((float)cos(a), (float)sin(a));
+            }
+            HIPCHK(hipMalloc(&h->d_tw_half, sizeof(c2) * (N / 2)));
+            HIPCHK(hipMemcpy(h->d_tw_half, twh.data(), sizeof(c2) * (N / 2), hipMemcpyHostToDevice));
+        }
+        if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s))) return rc;
+        const int m = n - first;
+        constexpr int T = fft_T<LOG2N - 1>();
+        hipLaunchKernelGGL((k_dbg_cols<LOG2N>), dim3(m * N), dim3(2 * T),
+                           2 * sizeof(c2) * lds_complex<N / 2>(), s, h->d_G, h->g_stride, h->d_dbg,
+                           tex_stride, first, h->p.show_magnitude, h->p.show_phase, h->geo,
+                           h->d_tw_half);
+        HIPCHK(hipGetLastError());
+        const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+        const size_t tot = (size_t)m * h->W * h->H;
+        const dim3 grid((unsigned)((tot + 255) / 256));
+        if (fmt == MM_RGBA8)
+            hipLaunchKernelGGL((k_dbg_out<0>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
+                               first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
+        else
+            hipLaunchKernelGGL((k_dbg_out<1>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
+                               first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
+        HIPCHK(hipGetLastError());
+    }
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    if ((rc = launch_k1<LOG2N>(h, in + fb * (n - 1), 1, fmt, s))) return rc;
+    if ((rc = launch_k2<LOG2N>(h, 1, 1, nullptr, h->d_state, s))) return rc;
+    h->has_state = true;
+    return MM_OK;
+}
+
 template <int LOG2N>
 static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int fmt,
                      hipStream_t s)
@@ -325,6 +374,7 @@ static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     const int first = h->has_state ? 0 : 1;
     int rc;
     if (first) HIPCHK(hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s));
+    if (h->p.show_magnitude || h->p.show_phase) return run_debug<LOG2N>(h, in, out, n, first, fmt, s);
     if (!h->p.apply_magnification) {
         // applyMotionMagnification == false: Blit(source, destination) (.cs:139),
         // but previousSourceTexture still follows the input (.cs:142).
@@ -440,6 +490,8 @@ int mm_params_default(mm_params *p)
     p->motion_sensitivity = 1.5f;  // .cs:41
     p->enhance_edges = 1;
     p->edge_enhancement = 0.8f;    // .cs:43
+    p->show_magnitude = 0;         // .cs:13
+    p->show_phase = 0;             // .cs:14
     return MM_OK;
 }
 
@@ -466,6 +518,8 @@ static void free_handle(mm_handle *h)
     (void)hipFree(h->d_col3);
     (void)hipFree(h->d_row3);
     (void)hipFree(h->d_tw);
+    (void)hipFree(h->d_tw_half);
+    (void)hipFree(h->d_dbg);
     (void)hipFree(h->d_G);
     (void)hipFree(h->d_Q);
     (void)hipFree(h->d_Yh);
@@ -620,7 +674,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     int rc = validate_params(p);
     if (rc) return rc;
     const bool edge_changed = p->edge_mode != h->p.edge_mode;
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipDeviceSynchronize());   // in-flight work on any stream may read the tables
     h->p = *p;
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
@@ -651,7 +705,7 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
     if (!h || !in || !out || count < 0) return MM_ERR_INVALID;
     if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
     if (count == 0) return MM_OK;
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     HIPCHK(hipSetDevice(h->device));
     return do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
 }
@@ -701,7 +755,7 @@ int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
     size_t need = 0;
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     if (!h->has_state) return MM_ERR_NO_STATE;
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     HIPCHK(hipMemcpyAsync(dev_buf, h->d_state, need, hipMemcpyDeviceToDevice, s));
     return MM_OK;
 }
@@ -710,7 +764,7 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
 {
     size_t need = 0;
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     HIPCHK(hipMemcpyAsync(h->d_state, dev_buf, need, hipMemcpyDeviceToDevice, s));
     h->has_state = true;
     return MM_OK;
@@ -722,7 +776,7 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
     size_t need = 0;
     if (!h || !in_dev || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     HIPCHK(hipSetDevice(h->device));
     return do_compute_state(h, (const uint8_t *)in_dev, format, (c2 *)dev_buf, s);
 }
@@ -731,7 +785,7 @@ void mm_destroy(mm_handle *h)
 {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    (void)hipStreamSynchronize(h->stream);
+    (void)hipDeviceSynchronize();   // work on caller streams may still use the buffers
     free_handle(h);
 }
 

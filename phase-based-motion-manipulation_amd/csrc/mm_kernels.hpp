@@ -814,6 +814,95 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
 }
 
 // =========================================================================
+// f3 debug views: ProcessDebugView (.cs:234-257)
+// =========================================================================
+// The reference shows complexBuffer1 after PerformFFT, which its ping-pong
+// (.cs:517-549) leaves one radix-2 column stage short of the spectrum: with
+// R[r][kx] = (-1)^r Frow[r][(kx + N/2) mod N] (centred, row-transformed), rows
+// [0, N/2) hold the N/2-point column DFT of the even rows r = 2m and rows
+// [N/2, N) that of the odd rows (oracle mm_ref_fft_buffer1, tests/np_twin.py).
+// One WG per (frame, column kx): group 0 transforms the even rows, group 1 the
+// odd rows (T/2 threads each, N/2-point FFT).  Frow comes from K1's half
+// spectra G (Hermitian: Frow[r][f] = conj G[N-f][r] for f > N/2; rows outside
+// the image are zero).  Chunk frame fr = frame0 + blockIdx / N reads G[fr] and
+// writes view texture fr - frame0.  Writes the log-magnitude view
+// (ConvertComplexMagToTexScaled, FFT.compute:152-161) and/or the phase view
+// (ConvertComplexPhaseToTex, :164-172) as N x N float textures.
+template <int LOG2N>
+__global__ __launch_bounds__(2 * fft_T<LOG2N - 1>())
+void k_dbg_cols(const c2 *__restrict__ G, size_t g_stride, float *__restrict__ tex,
+                size_t tex_stride, int frame0, int want_mag, int want_phase, Geo g,
+                const c2 *__restrict__ tw_half)
+{
+    constexpr int N = 1 << LOG2N, M = N / 2, T = fft_T<LOG2N - 1>();
+    extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
+    const int grp = threadIdx.x / T, t = threadIdx.x % T;   // 0: even rows, 1: odd rows
+    c2 *lds = lds_all + grp * lds_complex<M>();
+    const int kx = blockIdx.x % N, fr = frame0 + blockIdx.x / N;
+    const int f = (kx + N / 2) & (N - 1);
+    const bool mirror = f > N / 2;
+    const c2 *Gc = G + (size_t)fr * g_stride + (size_t)(mirror ? N - f : f) * g.H;
+    const float sgn = grp ? -1.0f : 1.0f;                     // (-1)^r
+    c2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int r = 2 * (t + j * T) + grp;                   // canvas row
+        const int rr = r - g.y0;
+        const c2 a = Gc[min(max(rr, 0), g.H - 1)];
+        const bool in = rr >= 0 && rr < g.H;
+        v[j] = in ? mk(sgn * a.x, sgn * (mirror ? -a.y : a.y)) : mk(0.0f, 0.0f);
+    }
+    fft_regs<LOG2N - 1, -1>(v, t, lds, tw_half);
+    float *mag = tex + (size_t)(fr - frame0) * tex_stride;
+    float *pha = mag + (size_t)N * N;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int row = grp * M + t + j * T;
+        const float m2 = v[j].x * v[j].x + v[j].y * v[j].y;
+        if (want_mag) mag[(size_t)row * N + kx] = __log10f(__builtin_amdgcn_sqrtf(m2) * 10.0f + 1.0f) * 0.25f;
+        if (want_phase) pha[(size_t)row * N + kx] = fabsf(atan2f(v[j].y, v[j].x)) * (1.0f / 1.57079632679f);
+    }
+}
+
+// CropTexture (.cs:386-410) of one view, or ShowSplitScreen (.cs:458-487) of
+// both (each N x N texture drawn bilinearly into one half).  RFloat textures
+// sample as (v, 0, 0, 1).
+template <int FMT>
+__global__ __launch_bounds__(256)
+void k_dbg_out(const float *__restrict__ tex, size_t tex_stride, uint8_t *__restrict__ frames_out,
+               size_t frame_bytes, int frame0, int nframes, int show_mag, int show_phase, Geo g)
+{
+    const size_t npx = (size_t)g.W * g.H;
+    const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (e >= npx * nframes) return;
+    const int k = (int)(e / npx);
+    const int p = (int)(e - (size_t)k * npx);
+    const int Y = p / g.W, X = p - Y * g.W;
+    const float *mag = tex + (size_t)k * tex_stride, *pha = mag + (size_t)g.N * g.N;
+    float v;
+    if (show_mag && show_phase) {
+        const bool right = 2 * X + 1 >= g.W;
+        const float u = (float)(2 * X + 1 - (right ? g.W : 0)) / (float)g.W;
+        const float vv = (float)(2 * Y + 1) / (float)(2 * g.H);
+        const float *tx = right ? pha : mag;
+        // bilinear at texel (u N - 0.5, v N - 0.5), sampler wrap = edge mode
+        const float sx = u * (float)g.N - 0.5f, sy = vv * (float)g.N - 0.5f;
+        const float fx0 = floorf(sx), fy0 = floorf(sy);
+        const float ax = sx - fx0, ay = sy - fy0;
+        const int ix = (int)fx0, iy = (int)fy0;
+        const int xa = wrap_idx(ix, g.N, g.edge), xb = wrap_idx(ix + 1, g.N, g.edge);
+        const int ya = wrap_idx(iy, g.N, g.edge), yb = wrap_idx(iy + 1, g.N, g.edge);
+        const float a = (1.0f - ax) * tx[(size_t)ya * g.N + xa] + ax * tx[(size_t)ya * g.N + xb];
+        const float b = (1.0f - ax) * tx[(size_t)yb * g.N + xa] + ax * tx[(size_t)yb * g.N + xb];
+        v = (1.0f - ay) * a + ay * b;
+    } else {
+        v = (show_mag ? mag : pha)[(size_t)(g.y0 + Y) * g.N + g.x0 + X];
+    }
+    if (FMT == 0) v = sat(v);   // UNORM destination
+    Pix<FMT>::store(frames_out + (size_t)(frame0 + k) * frame_bytes, (unsigned)p, v, 0.0f, 0.0f);
+}
+
+// =========================================================================
 // synthetic stream, RGBA8
 // =========================================================================
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x)

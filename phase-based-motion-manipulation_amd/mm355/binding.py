@@ -41,15 +41,17 @@ class Params(ctypes.Structure):
                 ("apply_bandpass_filter", ctypes.c_int), ("low_frequency_cutoff", ctypes.c_float),
                 ("high_frequency_cutoff", ctypes.c_float), ("filter_steepness", ctypes.c_float),
                 ("motion_sensitivity", ctypes.c_float), ("enhance_edges", ctypes.c_int),
-                ("edge_enhancement", ctypes.c_float)]
+                ("edge_enhancement", ctypes.c_float),
+                ("show_magnitude", ctypes.c_int), ("show_phase", ctypes.c_int)]
 
     @classmethod
     def make(cls, levels=5, min_freq=0.05, max_freq=0.45, phase_scale=10.0,
              magnitude_threshold=0.01, edge_mode=EDGE_REPEAT, apply_magnification=True,
              mode=MODE_PYRAMID, **standard):
-        """standard-mode fields (mm.h) by keyword: apply_bandpass_filter,
-        low_frequency_cutoff, high_frequency_cutoff, filter_steepness,
-        motion_sensitivity, enhance_edges, edge_enhancement."""
+        """other mm.h fields by keyword: the standard-mode band-pass
+        (apply_bandpass_filter, low_frequency_cutoff, high_frequency_cutoff,
+        filter_steepness, motion_sensitivity, enhance_edges, edge_enhancement)
+        and the debug views (show_magnitude, show_phase)."""
         p = cls()
         lib().mm_params_default(ctypes.byref(p))
         p.levels, p.min_freq, p.max_freq = levels, min_freq, max_freq
@@ -59,11 +61,13 @@ class Params(ctypes.Structure):
         for k, v in standard.items():
             if k not in dict(cls._fields_):
                 raise TypeError(f"unknown mm_params field {k}")
-            setattr(p, k, int(v) if k in ("apply_bandpass_filter", "enhance_edges") else v)
+            setattr(p, k, int(v) if k in ("apply_bandpass_filter", "enhance_edges",
+                                          "show_magnitude", "show_phase") else v)
         return p
 
 
 _lib = None
+ABI_VERSION = 3   # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):
@@ -106,6 +110,11 @@ def load_library(path=None):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    # mm_params grows only at its end: an older library (ABI >= 2) reads a prefix
+    # of Params (A/B builds); a newer one than this binding is refused.
+    abi = L.mm_abi_version()
+    if abi > ABI_VERSION or abi < 2:
+        raise MMError(-1, f"{path}: ABI {abi}, binding expects <= {ABI_VERSION}")
     _lib = L
     return L
 

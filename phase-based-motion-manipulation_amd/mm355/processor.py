@@ -59,8 +59,6 @@ class MotionMagnificationProcessor:
 
     # -- reference lifecycle -------------------------------------------------
     def _params(self):
-        if self.show_magnitude or self.show_phase:
-            raise MMError(-2, "debug views (.cs:234-257) are out of scope")
         # usePyramidDecomposition selects ProcessFrameWithPyramidDecomposition or
         # ProcessFrameWithStandardMagnification (.cs:128-135)
         mode = MODE_PYRAMID if self.use_pyramid_decomposition else MODE_STANDARD
@@ -75,7 +73,9 @@ class MotionMagnificationProcessor:
                            filter_steepness=self.filter_steepness,
                            motion_sensitivity=self.motion_sensitivity,
                            enhance_edges=self.enhance_edges,
-                           edge_enhancement=self.edge_enhancement)
+                           edge_enhancement=self.edge_enhancement,
+                           # showMagnitude / showPhase: ProcessDebugView (.cs:119-123)
+                           show_magnitude=self.show_magnitude, show_phase=self.show_phase)
 
     def Start(self):
         """Start -> InitializeProcessor (.cs:90-94, :289-342). Raises on failure."""
@@ -89,8 +89,8 @@ class MotionMagnificationProcessor:
 
     def OnRenderImage(self, source, destination):
         """OnRenderImage (.cs:101-143). source/destination: [H, W, 4] uint8 or
-        float32, both torch CUDA tensors (async on the handle's stream) or both
-        host numpy arrays (synchronous)."""
+        float32, both torch CUDA tensors (async on torch's current stream) or
+        both host numpy arrays (synchronous)."""
         if self._handle is None:                       # !isInitialized -> Blit (.cs:103-107)
             destination[...] = source
             return
@@ -105,7 +105,11 @@ class MotionMagnificationProcessor:
                 raise MMError(-1, "frames must be C-contiguous")
         elif not (source.is_contiguous() and destination.is_contiguous()):
             raise MMError(-1, "frames must be contiguous")
-        self._handle.process(source, destination, fmt, on_device=on_dev)
+        stream = None
+        if on_dev:   # order after whatever produced `source` on torch's current stream
+            import torch
+            stream = torch.cuda.current_stream(source.device).cuda_stream
+        self._handle.process(source, destination, fmt, on_device=on_dev, stream=stream)
 
     def OnDestroy(self):
         """OnDestroy -> ReleaseResources (.cs:96-99, :344-356)."""

@@ -28,20 +28,24 @@ def _std_fields(std):
 
 
 def oracle_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, apply=True,
-               standard=None):
+               standard=None, debug=None):
     o = O.Oracle(W, H, levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
                  edge_mode=edge)
     o.set_apply(apply)
     if standard is not None:
         o.set_standard(True, **standard)
+    if debug is not None:
+        o.set_debug(*debug)
     return [o.process(f) for f in frames]
 
 
 def gpu_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, mode="frame",
-            apply=True, standard=None):
+            apply=True, standard=None, debug=None):
     import torch
     import mm355
     extra = {} if standard is None else dict(mode=mm355.MODE_STANDARD, **_std_fields(standard))
+    if debug is not None:
+        extra.update(show_magnitude=debug[0], show_phase=debug[1])
     p = mm355.Params.make(levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
                           edge_mode=edge, apply_magnification=apply, **extra)
     h = mm355.Handle(W, H, p)

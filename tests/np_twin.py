@@ -192,3 +192,39 @@ def process_frame(cur, prev, L, minf, maxf, S, tau=0.01, edge=0, dbg=None, stand
     if dbg is not None:
         dbg.update(y_cur=pc[..., 0], F_cur=Fc, F_prev=Fp, A=acc, y_mag=ymag, y_blur=yb)
     return out
+
+
+def debug_buffer1(y):
+    """complexBuffer1 after PerformFFT, formulated independently of the radix-2
+    ping-pong: centred rows transformed along x, then the N/2-point column DFTs
+    of the even rows (rows [0, N/2)) and of the odd rows (rows [N/2, N)) -- the
+    state one radix-2 DIT stage before the full column transform."""
+    N = y.shape[0]
+    sgn = np.where((np.add.outer(np.arange(N), np.arange(N)) & 1) == 1, -1.0, 1.0)
+    r = np.fft.fft(y * sgn, axis=1)
+    return np.vstack([np.fft.fft(r[0::2], axis=0), np.fft.fft(r[1::2], axis=0)])
+
+
+def debug_view(frame, N, edge, show_mag, show_phase):
+    """ProcessDebugView (.cs:234-257) in float64: RFloat view textures sampled
+    as (v, 0, 0, 1); crop for one view, bilinear split screen for both."""
+    H, W = frame.shape[:2]
+    y = pad_window(frame, N, edge)[..., 0]
+    b = debug_buffer1(y)
+    mag = np.log10(np.abs(b) * 10.0 + 1.0) / 4.0
+    pha = np.abs(np.angle(b)) / 1.57079632679
+    out = np.zeros((H, W, 4))
+    out[..., 3] = 1.0
+    if show_mag and show_phase:
+        X = np.arange(W)
+        right = 2 * X + 1 >= W
+        u = (2 * X + 1 - np.where(right, W, 0)) / W
+        v = (2 * np.arange(H) + 1) / (2.0 * H)
+        UU, VV = np.meshgrid(u, v)
+        lm = _bilinear(mag[..., None], UU, VV, edge)[..., 0]
+        lp = _bilinear(pha[..., None], UU, VV, edge)[..., 0]
+        out[..., 0] = np.where(right[None, :], lp, lm)
+    else:
+        x0, y0 = (N - W) // 2, (N - H) // 2
+        out[..., 0] = (mag if show_mag else pha)[y0:y0 + H, x0:x0 + W]
+    return out

@@ -71,6 +71,8 @@ def lib():
         L.mm_ref_blur.argtypes = [ctypes.c_int, ctypes.c_int, fp]
         L.mm_ref_synth_frame.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_uint64, ctypes.c_int, u8p]
+        L.mm_ref_set_debug.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.mm_ref_fft_buffer1.argtypes = [ctypes.c_int, fp, fp]
         L.mm_ref_set_threads.argtypes = [ctypes.c_int]
         L.mm_ref_set_threads.restype = ctypes.c_int
         _lib = L
@@ -102,6 +104,15 @@ def fft_centered(y):
     n = y.shape[0]
     out = np.empty((n, n, 2), np.float32)
     lib().mm_ref_fft_centered(n, _fp(y), _fp(out))
+    return out[..., 0] + 1j * out[..., 1].astype(np.complex64)
+
+
+def fft_buffer1(y):
+    """complexBuffer1 after PerformFFT (what ProcessDebugView reads)."""
+    y = np.ascontiguousarray(y, np.float32)
+    n = y.shape[0]
+    out = np.empty((n, n, 2), np.float32)
+    lib().mm_ref_fft_buffer1(n, _fp(y), _fp(out))
     return out[..., 0] + 1j * out[..., 1].astype(np.complex64)
 
 
@@ -182,6 +193,10 @@ class Oracle:
         """usePyramidDecomposition = false; edge = enhanceEdges ? edgeEnhancement : 0."""
         lib().mm_ref_set_standard(self.h, 1 if on else 0, 1 if apply else 0, low, high, steep,
                                   sens, edge)
+
+    def set_debug(self, show_magnitude=False, show_phase=False):
+        """showMagnitude / showPhase (.cs:13-14): ProcessDebugView output."""
+        lib().mm_ref_set_debug(self.h, 1 if show_magnitude else 0, 1 if show_phase else 0)
 
     def reset(self):
         lib().mm_ref_reset(self.h)

@@ -236,3 +236,132 @@ def test_processor_standard_mode():
     for k in range(1, 3):
         T.assert_close_f32(dst[k].cpu().numpy(), ref[k])
     proc.OnDestroy()
+
+
+# ---- f3 debug views (ProcessDebugView .cs:234-257) ---------------------------
+
+def _debug_close(got, ref, mag_only):
+    """R channel.  |spectrum| view log10(10|z|+1)/4: slope <= 1.09 near |z| = 0
+    and the fp32 FFT error is absolute (~1e-7 of the spectrum's peak), so
+    max <= 1e-4 and 99.9th percentile <= 1e-5.  The |phase| view's error is
+    (FFT absolute error) / |z|, unbounded as |z| -> 0 (where even the sign of a
+    tiny imaginary part flips): median <= 5e-6 and 99.9th percentile <= 2e-4
+    (measured 1.0e-6 and 5.2e-5 at 200x120).  G = B = 0, alpha 1."""
+    assert np.array_equal(got[..., 1:3], np.zeros_like(got[..., 1:3]))
+    assert np.all(got[..., 3] == 1.0)
+    e = np.abs(got[..., 0].astype(np.float64) - ref[..., 0])
+    if mag_only:
+        assert e.max() < 1e-4 and np.quantile(e, 0.999) < 1e-5, (e.max(), np.quantile(e, 0.999))
+    else:
+        assert np.quantile(e, 0.999) < 2e-4 and np.median(e) < 5e-6, (np.quantile(e, 0.999), e.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("view", [(True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("W,H,edge", [(64, 48, 0), (200, 120, 1)])
+def test_debug_view_f32(view, W, H, edge):
+    fr = T.synth(W, H, 4)
+    ref = T.oracle_run(W, H, fr, edge=edge, debug=view)
+    got = T.gpu_run(W, H, fr, edge=edge, mode="stream", debug=view)
+    assert np.array_equal(got[0], fr[0])
+    for k in range(1, 4):
+        _debug_close(got[k], ref[k], view == (True, False))
+
+
+@pytest.mark.gpu
+def test_debug_view_u8_and_state():
+    """RGBA8 output (saturated R, alpha 255); after switching the view off the
+    magnified output matches the oracle (state followed the input)."""
+    import mm355
+    import torch
+    W, H = 96, 64
+    fr = T.synth(W, H, 4, fmt="u8")
+    o = O.Oracle(W, H, levels=5, phase_scale=10.0)
+    o.set_debug(True, False)
+    ref = [o.process(fr[0]), o.process(fr[1])]
+    o.set_debug(False, False)
+    ref += [o.process(fr[2]), o.process(fr[3])]
+    p = mm355.Params.make(levels=5, phase_scale=10.0, show_magnitude=True)
+    h = mm355.Handle(W, H, p)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    out = torch.empty_like(dev)
+    h.process(dev[0], out[0], mm355.RGBA8)
+    h.process(dev[1], out[1], mm355.RGBA8)
+    h.set_params(mm355.Params.make(levels=5, phase_scale=10.0))
+    h.process(dev[2], out[2], mm355.RGBA8)
+    h.process(dev[3], out[3], mm355.RGBA8)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    h.close()
+    assert np.array_equal(got[0], fr[0])
+    d = np.abs(got[1].astype(np.int32) - ref[1].astype(np.int32))
+    assert d.max() <= 1 and np.all(got[1][..., 1:3] == 0) and np.all(got[1][..., 3] == 255)
+    for k in (2, 3):
+        T.assert_close_u8(got[k], ref[k])
+
+
+@pytest.mark.gpu
+def test_processor_debug_view_toggle():
+    """showPhase via the mirror: OnValidate switches the view on and off."""
+    import mm355
+    W, H = 64, 48
+    fr = T.synth(W, H, 3)
+    ref = T.oracle_run(W, H, fr[:2], debug=(False, True))
+    proc = mm355.MotionMagnificationProcessor(W, H, show_phase=True, phase_scale=10.0)
+    proc.Start()
+    outs = []
+    for f in fr[:2]:
+        o = np.empty_like(f)
+        proc.OnRenderImage(f, o)
+        outs.append(o)
+    _debug_close(outs[1], ref[1], False)
+    proc.show_phase = False
+    proc.OnValidate()
+    o = np.empty_like(fr[2])
+    proc.OnRenderImage(fr[2], o)
+    ref2 = T.oracle_run(W, H, fr[1:3])
+    T.assert_close_f32(o, ref2[1])
+    proc.OnDestroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,t0,gray", [(64, 48, 0, False), (200, 120, 7, False), (96, 64, 3, True)])
+def test_device_synth_matches_oracle(W, H, t0, gray):
+    """mm_synth_frames (the bench's input generator) reproduces the oracle's
+    synthetic stream: exact except a +-1 step where the double-precision
+    sin/cos of device and host libm round v*255+0.5 to different sides."""
+    import mm355
+    import torch
+    h = mm355.Handle(W, H)
+    dev = torch.empty((3, H, W, 4), dtype=torch.uint8, device="cuda")
+    h.synth(dev, t0, 3, gray=gray)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    h.close()
+    ref = np.stack([O.synth_frame(W, H, t0 + k, gray=gray) for k in range(3)])
+    d = np.abs(got.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() <= 1 and (d > 0).mean() < 1e-4, (d.max(), (d > 0).mean())
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_1080p_stream_device_synth_u8():
+    """The bench's path end to end: device-generated 1080p RGBA8 stream, one
+    multi-frame mm_process_stream call on the default stream (ordered after
+    mm_synth_frames), crossing a chunk boundary; against the oracle."""
+    import mm355
+    import torch
+    W, H, n = 1920, 1080, 10
+    h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
+    fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    h.synth(fr, 0, n)
+    out = torch.empty_like(fr)
+    h.process_stream(fr, out, n, mm355.RGBA8)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    h.close()
+    O.set_threads(16)
+    ref = T.oracle_run(W, H, [O.synth_frame(W, H, t) for t in range(n)], levels=5, S=25.0)
+    assert np.array_equal(got[0], ref[0])
+    for k in range(1, n):
+        T.assert_close_u8(got[k], ref[k])

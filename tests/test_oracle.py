@@ -210,3 +210,53 @@ def test_standard_mode_static_scene_is_identity_spectrum():
         o.process(f)
         outs.append(o.process(f))
     assert np.abs(outs[0] - outs[1]).max() < 1e-6
+
+
+# ---- f3 debug views (ProcessDebugView, .cs:234-257) -------------------------
+
+def test_fft_buffer1_is_penultimate_column_stage():
+    """complexBuffer1 after the radix-2 ping-pong = even/odd-row N/2-point column
+    DFTs of the fully row-transformed, centred image (twin, np.fft)."""
+    for n in (16, 32, 256):
+        y = np.random.default_rng(n).standard_normal((n, n)).astype(np.float32)
+        b = O.fft_buffer1(y)
+        t = np_twin.debug_buffer1(y.astype(np.float64))
+        assert np.abs(b - t).max() / np.abs(t).max() < 2e-6
+        # and it is NOT the finished spectrum
+        assert np.abs(b - O.fft_centered(y)).max() > 1e-2 * np.abs(t).max()
+
+
+@pytest.mark.parametrize("mag,pha", [(True, False), (False, True), (True, True)])
+def test_debug_view_matches_twin(mag, pha):
+    W, H = 64, 48
+    f0, f1 = (O.synth_frame(W, H, t).astype(np.float32) / np.float32(255) for t in (0, 1))
+    o = O.Oracle(W, H, levels=5, phase_scale=10.0)
+    o.set_debug(mag, pha)
+    assert np.array_equal(o.process(f0), f0)          # first frame still passes through
+    out = o.process(f1)
+    ref = np_twin.debug_view(f1.astype(np.float64), o.N, 0, mag, pha)
+    assert np.array_equal(out[..., 1:3], np.zeros_like(out[..., 1:3]))
+    assert np.all(out[..., 3] == 1.0)
+    err = np.abs(out[..., 0] - ref[..., 0])
+    if mag and not pha:
+        assert err.max() < 1e-5
+    else:   # |arg z| is ill-conditioned where |z| ~ 0: judge by percentiles
+        assert np.quantile(err, 0.999) < 1e-4 and np.median(err) < 1e-6
+    o.close()
+
+
+def test_debug_view_state_follows_input():
+    """While a debug view is on, previousSourceTexture still follows the input
+    (.cs:122): switching it off magnifies against the last debug-view frame."""
+    W, H = 64, 48
+    fr = [O.synth_frame(W, H, t).astype(np.float32) / np.float32(255) for t in range(3)]
+    a = O.Oracle(W, H, levels=5, phase_scale=10.0)
+    b = O.Oracle(W, H, levels=5, phase_scale=10.0)
+    a.process(fr[0])
+    a.set_debug(True, False)
+    a.process(fr[1])
+    a.set_debug(False, False)
+    b.process(fr[1])
+    assert np.array_equal(a.process(fr[2]), b.process(fr[2]))
+    a.close()
+    b.close()
