@@ -3,11 +3,16 @@
  *
  * Plays the role of the Unity camera that calls OnRenderImage once per frame
  * (Assets/Scripts/MotionMagnificationProcessor.cs:101): it generates a
- * synthetic RGBA8 stream on the device, runs the magnifier over
- * it and reports throughput.  Optional raw RGBA8 file I/O for real clips.
+ * synthetic RGBA8 stream on the device, or reads a clip, runs
+ * the magnifier over it and reports throughput.
  *
  *   mm_cli [-w W] [-h H] [-n frames] [-l levels] [-s phase_scale]
- *          [-b frames_per_call] [-i in.rgba] [-o out.rgba] [-d device]
+ *          [-b frames_per_call] [-i in.{rgba,y4m}] [-o out.{rgba,y4m}] [-d device]
+ *          [--full-range] [--standard] [--show-magnitude] [--show-phase]
+ *
+ * .y4m input: 8-bit 4:2:0 / 4:4:4 / mono YUV4MPEG2, geometry from its header
+ * (host/y4m.h, BT.601 limited range unless --full-range); .y4m output is 4:4:4
+ * at the input's frame rate.  Any other extension is raw RGBA8 (-w/-h).
  */
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
@@ -15,6 +20,7 @@
 #include <string.h>
 
 #include "mm.h"
+#include "y4m.h"
 
 #define CHECK(x)                                                                      \
     do {                                                                              \
@@ -25,13 +31,24 @@
         }                                                                             \
     } while (0)
 
+static int ends_with(const char *s, const char *suf)
+{
+    const size_t n = strlen(s), m = strlen(suf);
+    return n >= m && strcmp(s + n - m, suf) == 0;
+}
+
 int main(int argc, char **argv)
 {
     int W = 1920, H = 1080, F = 300, L = 5, B = 30, dev = 0;
+    int full_range = 0, standard = 0, show_mag = 0, show_phase = 0;
     float S = 25.0f;
     const char *in_path = NULL, *out_path = NULL;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
+        if (!strcmp(a, "--full-range")) { full_range = 1; continue; }
+        if (!strcmp(a, "--standard")) { standard = 1; continue; }
+        if (!strcmp(a, "--show-magnitude")) { show_mag = 1; continue; }
+        if (!strcmp(a, "--show-phase")) { show_phase = 1; continue; }
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
         if (!v) { fprintf(stderr, "missing value for %s\n", a); return 2; }
         if (!strcmp(a, "-w")) W = atoi(v);
@@ -47,10 +64,26 @@ int main(int argc, char **argv)
         ++i;
     }
     if (B < 1) B = 1;
+    FILE *fi = in_path ? fopen(in_path, "rb") : NULL;
+    FILE *fo = out_path ? fopen(out_path, "wb") : NULL;
+    if ((in_path && !fi) || (out_path && !fo)) { fprintf(stderr, "cannot open file\n"); return 1; }
+    const int y4m_in = in_path && ends_with(in_path, ".y4m");
+    const int y4m_out = out_path && ends_with(out_path, ".y4m");
+    y4m_info yi = {0};
+    yi.fps_num = 25;
+    yi.fps_den = 1;
+    if (y4m_in) {
+        if (y4m_read_header(fi, &yi)) { fprintf(stderr, "%s: unsupported Y4M\n", in_path); return 1; }
+        W = yi.width;
+        H = yi.height;
+    }
     mm_params p;
     mm_params_default(&p);
     p.levels = L;
     p.phase_scale = S;
+    p.mode = standard ? MM_MODE_STANDARD : MM_MODE_PYRAMID;
+    p.show_magnitude = show_mag;
+    p.show_phase = show_phase;
     mm_handle *h = NULL;
     CHECK(mm_create(W, H, &p, dev, &h));
     int N = 0;
@@ -64,10 +97,16 @@ int main(int argc, char **argv)
         return 1;
     }
     hipStream_t s = (hipStream_t)mm_stream(h);
-    FILE *fi = in_path ? fopen(in_path, "rb") : NULL;
-    FILE *fo = out_path ? fopen(out_path, "wb") : NULL;
-    if ((in_path && !fi) || (out_path && !fo)) { fprintf(stderr, "cannot open file\n"); return 1; }
     unsigned char *host = (fi || fo) ? (unsigned char *)malloc(fb * B) : NULL;
+    unsigned char *planes = (y4m_in || y4m_out)
+        ? (unsigned char *)malloc(y4m_in ? (y4m_frame_bytes(&yi) > 3 * (size_t)W * H
+                                               ? y4m_frame_bytes(&yi) : 3 * (size_t)W * H)
+                                         : 3 * (size_t)W * H)
+        : NULL;
+    if (y4m_out && y4m_write_header(fo, W, H, yi.fps_num, yi.fps_den)) {
+        fprintf(stderr, "write failed\n");
+        return 1;
+    }
 
     double t_proc = 0.0;
     int done = 0;
@@ -76,7 +115,18 @@ int main(int argc, char **argv)
     hipEventCreate(&e1);
     while (done < F) {
         int n = F - done < B ? F - done : B;
-        if (fi) {
+        if (fi && y4m_in) {
+            int got = 0;
+            for (; got < n; ++got) {
+                const int r = y4m_read_frame(fi, &yi, planes);
+                if (r < 0) { fprintf(stderr, "%s: malformed frame\n", in_path); return 1; }
+                if (r == 0) break;
+                y4m_to_rgba(&yi, planes, host + fb * got, full_range);
+            }
+            if (got == 0) break;
+            n = got;
+            hipMemcpyAsync(d_in, host, fb * n, hipMemcpyHostToDevice, s);
+        } else if (fi) {
             size_t got = fread(host, fb, (size_t)n, fi);
             if (got == 0) break;
             n = (int)got;
@@ -93,7 +143,14 @@ int main(int argc, char **argv)
         if (done > 0) t_proc += ms * 1e-3;      /* first call holds the passthrough frame */
         if (fo) {
             hipMemcpy(host, d_out, fb * n, hipMemcpyDeviceToHost);
-            fwrite(host, fb, (size_t)n, fo);
+            if (y4m_out) {
+                for (int k = 0; k < n; ++k) {
+                    y4m_from_rgba(W, H, host + fb * k, planes, full_range);
+                    if (y4m_write_frame(fo, W, H, planes)) { fprintf(stderr, "write failed\n"); return 1; }
+                }
+            } else {
+                fwrite(host, fb, (size_t)n, fo);
+            }
         }
         done += n;
     }
@@ -106,6 +163,7 @@ int main(int argc, char **argv)
     if (fi) fclose(fi);
     if (fo) fclose(fo);
     free(host);
+    free(planes);
     hipFree(d_in);
     hipFree(d_out);
     mm_destroy(h);
