@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 3
+#define MM_ABI_VERSION 4
 
 /* error codes */
 #define MM_OK               0
@@ -49,6 +49,9 @@ extern "C" {
 /* mm_params.mode */
 #define MM_MODE_PYRAMID   0   /* usePyramidDecomposition = true (.cs:18, :128-131) */
 #define MM_MODE_STANDARD  1   /* usePyramidDecomposition = false (.cs:132-135, :208-232) */
+#define MM_MODE_STEERABLE 2  /* extension f2: oriented local-phase subbands + temporal filter */
+#define MM_FILTER_DIFF 0      /* steerable: the reference's 2-tap phase difference per coefficient */
+#define MM_FILTER_IIR  1      /* steerable: band-pass IIR of the unwrapped local phase */
 /* mm_params.edge_mode: sampler wrap of the engine resamples and the blur
  * (unpinned by the reference) */
 #define MM_EDGE_REPEAT 0
@@ -84,6 +87,15 @@ typedef struct {
      * follows the input (.cs:122).  Since ABI 3. */
     int   show_magnitude;         /* showMagnitude        .cs:13 */
     int   show_phase;             /* showPhase            .cs:14 */
+    /* MM_MODE_STEERABLE (extension; spec oracle/steerable_ref.py;
+     * no reference counterpart): `orientations` in {4, 6, 8} oriented cos^4
+     * subbands per middle level, local phase filtered per coefficient by
+     * `temporal_filter` (MM_FILTER_DIFF | MM_FILTER_IIR with first-order
+     * low-pass coefficients iir_low < iir_high in (0, 1]), amplified by
+     * phase_scale; magnitude_threshold gates |subband| < tau.  Since ABI 4. */
+    int   temporal_filter;
+    float iir_low;
+    float iir_high;
 } mm_params;
 
 /* Reference defaults (.cs:12-43): levels 5, 0.05/0.45, phaseScale 10, threshold

@@ -20,6 +20,7 @@
 
 #include "../../include/mm.h"
 #include "mm_kernels_w.hpp"
+#include "mm_steer.hpp"
 
 using namespace mm;
 
@@ -46,6 +47,12 @@ struct mm_handle {
     c2 *d_tw;
     c2 *d_tw_half;              // W_{N/2} table (debug views, lazily)
     float *d_dbg;               // debug view textures [chunk][mag, phase][N][N] (lazily)
+    // MM_MODE_STEERABLE (lazily, for the current levels/orientations):
+    c2 *d_Fb;                   // per chunk frame half spectrum [chunk][N/2+1][N]
+    c2 *d_T;                    // band columns [nb+1][N][Hq]
+    float *d_sst;               // temporal-filter state: phi, u_h, u_l planes [nb][Hn][W+4]
+    int steer_nb;               // bands the steerable buffers were sized for (-1: none)
+    bool steer_valid;           // d_sst holds the state after the previous frame
     c2 *d_G, *d_Q, *d_state;
     float *d_Yh;
     size_t g_stride, q_stride, yh_stride;  // elements per frame
@@ -164,6 +171,16 @@ static void build_spec(const mm_params &p, int N, Spec &sp)
     sp.hp_inv = 1.0f / (p.max_freq * 0.2f);
     sp.lp_hi = p.min_freq * 1.2f;             // PyramidOperations.compute:48-53
     sp.lp_inv = 1.0f / (p.min_freq * 0.2f);
+    // steerable extension (mm_steer.hpp)
+    sp.O = p.mode == MM_MODE_STEERABLE ? p.orientations : 1;
+    sp.filt = p.temporal_filter;
+    sp.r_low = p.iir_low;
+    sp.r_high = p.iir_high;
+    for (int k = 0; k < 8; ++k) {
+        const double a = k < sp.O ? 2.0 * M_PI * k / sp.O : 0.0;
+        sp.ang_c[k] = (float)cos(a);
+        sp.ang_s[k] = (float)sin(a);
+    }
     for (int i = 1; i < p.levels - 1; ++i) {
         // PyramidOperations.compute:59-64 (L=3: 0/0 = NaN -> empty band)
         volatile float num = (float)(i - 1), den = (float)(p.levels - 3);
@@ -207,8 +224,20 @@ static int validate_params(const mm_params *p)
 {
     if (!p) return MM_ERR_INVALID;
     if (p->levels < 1 || p->levels > kMaxLevels) return MM_ERR_UNSUPPORTED;
-    if (p->orientations != 1) return MM_ERR_UNSUPPORTED;
-    if (p->mode != MM_MODE_PYRAMID && p->mode != MM_MODE_STANDARD) return MM_ERR_UNSUPPORTED;
+    if (p->mode == MM_MODE_STEERABLE) {
+        // cos^4 lobes cover every direction from 4 orientations up; even O pairs
+        // each lobe with its conjugate mirror (oracle/steerable_ref.py)
+        if (p->orientations != 4 && p->orientations != 6 && p->orientations != 8)
+            return MM_ERR_UNSUPPORTED;
+        if (p->temporal_filter != MM_FILTER_DIFF && p->temporal_filter != MM_FILTER_IIR)
+            return MM_ERR_INVALID;
+        if (p->temporal_filter == MM_FILTER_IIR &&
+            !(p->iir_low > 0.0f && p->iir_low < p->iir_high && p->iir_high <= 1.0f))
+            return MM_ERR_INVALID;
+    } else {
+        if (p->orientations != 1) return MM_ERR_UNSUPPORTED;
+        if (p->mode != MM_MODE_PYRAMID && p->mode != MM_MODE_STANDARD) return MM_ERR_UNSUPPORTED;
+    }
     if (p->edge_mode != MM_EDGE_REPEAT && p->edge_mode != MM_EDGE_CLAMP) return MM_ERR_INVALID;
     if (!(p->min_freq > 0.0f) || !(p->max_freq > 0.0f)) return MM_ERR_INVALID;
     return MM_OK;
@@ -287,6 +316,9 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     return MM_OK;
 }
 
+static int launch_k4(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, int nframes,
+                     int fmt, hipStream_t s);
+
 template <int LOG2N>
 static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, int nframes,
                      int fmt, hipStream_t s)
@@ -304,6 +336,15 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
                            h->blur, h->d_tw);
         HIPCHK(hipGetLastError());
     }
+    return launch_k4(h, in, out, frame0, nframes, fmt, s);
+}
+
+// K4 k_compose over chunk frames [frame0, nframes) (Yh of those frames ready)
+static int launch_k4(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, int nframes,
+                     int fmt, hipStream_t s)
+{
+    const int nout = nframes - frame0;
+    if (nout <= 0) return MM_OK;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     const int rt = (h->H + kTileRows - 1) / kTileRows, ct = (h->W + kTileCols - 1) / kTileCols;
     const dim3 grid(rt * ct * nout);
@@ -316,6 +357,89 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
                            in, out, fb, frame0, rt, ct, h->geo, h->blur, h->d_col3, h->d_row3);
     HIPCHK(hipGetLastError());
     return MM_OK;
+}
+
+// ---- MM_MODE_STEERABLE (mm_steer.hpp) -----------------------------------
+static int steer_bands(const mm_handle *h)
+{
+    const int nmid = h->spec.L >= 3 ? h->spec.L - 2 : 0;
+    return nmid * (h->spec.O / 2);
+}
+static size_t steer_state_bytes(const mm_handle *h)
+{
+    return sizeof(float) * 3 * (size_t)steer_bands(h) * h->geo.Hn * (h->W + 4);
+}
+static int steer_alloc(mm_handle *h)
+{
+    const int nb = steer_bands(h);
+    if (h->steer_nb == nb) return MM_OK;
+    (void)hipFree(h->d_Fb);
+    (void)hipFree(h->d_T);
+    (void)hipFree(h->d_sst);
+    h->d_Fb = h->d_T = nullptr;
+    h->d_sst = nullptr;
+    h->steer_nb = -1;
+    h->steer_valid = false;
+    const size_t fstride = (size_t)(h->N / 2 + 1) * h->N;
+    if (hipMalloc(&h->d_Fb, sizeof(c2) * fstride * h->chunk) != hipSuccess ||
+        hipMalloc(&h->d_T, sizeof(c2) * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
+        hipMalloc(&h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
+        return MM_ERR_OOM;
+    h->steer_nb = nb;
+    return MM_OK;
+}
+
+// Chunk frames [0, n): K1 -> k_cols_fwd -> per frame k_sb_cols, k_sb_rows (the
+// temporal filter runs frame by frame) -> K4.  The first `seed` frames (0 or
+// 1: no valid state after create/reset/mode change) pass through and seed it.
+// apply_magnification == false: output passes through, the state keeps
+// following the input.  `sst`: state planes (the handle's or a caller buffer).
+template <int LOG2N>
+static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int fmt, float *sst,
+                     bool write, int seed, hipStream_t s)
+{
+    constexpr int N = 1 << LOG2N;
+    int rc;
+    if ((rc = steer_alloc(h))) return rc;
+    if (!sst) sst = h->d_sst;
+    if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s))) return rc;
+    const size_t fstride = (size_t)(N / 2 + 1) * N;
+    const int gpw = groups_per_wg<LOG2N>();
+    const size_t lds = lds_fft_bytes<LOG2N>();
+    {
+        const int total = n * (N / 2 + 1);
+        ProfScope ps(h, s, MM_K_COLS, n);
+        hipLaunchKernelGGL((k_cols_fwd<LOG2N>), dim3((total + gpw - 1) / gpw),
+                           dim3(wg_threads<LOG2N>()), lds, s, h->d_G, h->g_stride, h->d_Fb,
+                           fstride, total, h->geo, h->d_tw);
+        HIPCHK(hipGetLastError());
+    }
+    const size_t band_stride = (size_t)N * h->geo.Hq;
+    const size_t plane = (size_t)steer_bands(h) * h->geo.Hn * (h->W + 4);
+    for (int k = 0; k < n; ++k) {
+        const int reset = k < seed;
+        {
+            ProfScope ps(h, s, MM_K_COLS, 0);
+            hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + gpw - 1) / gpw), dim3(wg_threads<LOG2N>()),
+                               lds, s, h->d_Fb + fstride * k, h->d_T, band_stride, h->geo, h->spec,
+                               h->d_tw);
+            HIPCHK(hipGetLastError());
+        }
+        ProfScope ps(h, s, MM_K_ROWS_INV, reset || !write ? 0 : 1);
+        hipLaunchKernelGGL((k_sb_rows<LOG2N>), dim3((h->geo.Hn + gpw - 1) / gpw),
+                           dim3(wg_threads<LOG2N>()), lds, s, h->d_T, band_stride,
+                           h->d_Yh + h->yh_stride * k, sst, sst + plane, sst + 2 * plane, reset,
+                           write && !reset ? 1 : 0, h->geo, h->spec, h->blur, h->d_tw);
+        HIPCHK(hipGetLastError());
+    }
+    if (sst == h->d_sst) h->steer_valid = true;
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    if (!write) {
+        if (out) HIPCHK(hipMemcpyAsync(out, in, fb * n, hipMemcpyDeviceToDevice, s));
+        return MM_OK;
+    }
+    if (seed) HIPCHK(hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s));
+    return launch_k4(h, in, out, seed, n, fmt, s);
 }
 
 // One batch of `n` consecutive frames (n <= chunk), all on the device.
@@ -374,7 +498,17 @@ static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     const int first = h->has_state ? 0 : 1;
     int rc;
     if (first) HIPCHK(hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s));
-    if (h->p.show_magnitude || h->p.show_phase) return run_debug<LOG2N>(h, in, out, n, first, fmt, s);
+    if (h->p.show_magnitude || h->p.show_phase) {
+        h->steer_valid = false;   // the debug path does not advance the local-phase state
+        return run_debug<LOG2N>(h, in, out, n, first, fmt, s);
+    }
+    if (h->p.mode == MM_MODE_STEERABLE) {
+        if (first) h->steer_valid = false;
+        rc = run_steer<LOG2N>(h, in, out, n, fmt, nullptr, h->p.apply_magnification != 0,
+                              h->steer_valid ? 0 : 1, s);
+        if (rc == MM_OK) h->has_state = true;
+        return rc;
+    }
     if (!h->p.apply_magnification) {
         // applyMotionMagnification == false: Blit(source, destination) (.cs:139),
         // but previousSourceTexture still follows the input (.cs:142).
@@ -412,6 +546,8 @@ template <int LOG2N>
 static int compute_state(mm_handle *h, const uint8_t *in, int fmt, c2 *dst, hipStream_t s)
 {
     int rc;
+    if (h->p.mode == MM_MODE_STEERABLE)   // DIFF: the local phases of this frame
+        return run_steer<LOG2N>(h, in, nullptr, 1, fmt, reinterpret_cast<float *>(dst), false, 1, s);
     if ((rc = launch_k1<LOG2N>(h, in, 1, fmt, s))) return rc;
     return launch_k2<LOG2N>(h, 1, 1, nullptr, dst, s);
 }
@@ -492,6 +628,9 @@ int mm_params_default(mm_params *p)
     p->edge_enhancement = 0.8f;    // .cs:43
     p->show_magnitude = 0;         // .cs:13
     p->show_phase = 0;             // .cs:14
+    p->temporal_filter = MM_FILTER_DIFF;
+    p->iir_low = 0.05f;
+    p->iir_high = 0.4f;
     return MM_OK;
 }
 
@@ -520,6 +659,9 @@ static void free_handle(mm_handle *h)
     (void)hipFree(h->d_tw);
     (void)hipFree(h->d_tw_half);
     (void)hipFree(h->d_dbg);
+    (void)hipFree(h->d_Fb);
+    (void)hipFree(h->d_T);
+    (void)hipFree(h->d_sst);
     (void)hipFree(h->d_G);
     (void)hipFree(h->d_Q);
     (void)hipFree(h->d_Yh);
@@ -662,6 +804,8 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
         return rc;
     }
     h->has_state = false;
+    h->steer_nb = -1;
+    h->steer_valid = false;
     if (getenv("MM_DEBUG"))
         fprintf(stderr, "mm355: Original: %dx%d, Padded: %dx%d\n", width, height, N, N);  // .cs:304
     *out = h;
@@ -675,6 +819,11 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     if (rc) return rc;
     const bool edge_changed = p->edge_mode != h->p.edge_mode;
     HIPCHK(hipDeviceSynchronize());   // in-flight work on any stream may read the tables
+    const mm_params &o = h->p;
+    if (p->mode != o.mode || p->levels != o.levels || p->orientations != o.orientations ||
+        p->temporal_filter != o.temporal_filter || p->min_freq != o.min_freq ||
+        p->max_freq != o.max_freq || p->edge_mode != o.edge_mode)
+        h->steer_valid = false;   // local-phase state of other bands / masks
     h->p = *p;
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
@@ -740,13 +889,15 @@ int mm_reset(mm_handle *h)
 {
     if (!h) return MM_ERR_INVALID;
     h->has_state = false;
+    h->steer_valid = false;
     return MM_OK;
 }
 
 int mm_state_size(const mm_handle *h, size_t *bytes)
 {
     if (!h || !bytes) return MM_ERR_INVALID;
-    *bytes = sizeof(c2) * (size_t)(h->N / 2 + 1) * h->N;
+    *bytes = h->p.mode == MM_MODE_STEERABLE ? steer_state_bytes(h)
+                                            : sizeof(c2) * (size_t)(h->N / 2 + 1) * h->N;
     return MM_OK;
 }
 
@@ -756,6 +907,11 @@ int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     if (!h->has_state) return MM_ERR_NO_STATE;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
+    if (h->p.mode == MM_MODE_STEERABLE) {
+        if (!h->steer_valid) return MM_ERR_NO_STATE;
+        HIPCHK(hipMemcpyAsync(dev_buf, h->d_sst, need, hipMemcpyDeviceToDevice, s));
+        return MM_OK;
+    }
     HIPCHK(hipMemcpyAsync(dev_buf, h->d_state, need, hipMemcpyDeviceToDevice, s));
     return MM_OK;
 }
@@ -765,6 +921,14 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
     size_t need = 0;
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
+    if (h->p.mode == MM_MODE_STEERABLE) {
+        int rc = steer_alloc(h);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(h->d_sst, dev_buf, need, hipMemcpyDeviceToDevice, s));
+        h->steer_valid = true;
+        h->has_state = true;
+        return MM_OK;
+    }
     HIPCHK(hipMemcpyAsync(h->d_state, dev_buf, need, hipMemcpyDeviceToDevice, s));
     h->has_state = true;
     return MM_OK;
@@ -778,6 +942,9 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
     if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     HIPCHK(hipSetDevice(h->device));
+    // the IIR state is a history of frames, not a function of one input frame
+    if (h->p.mode == MM_MODE_STEERABLE && h->p.temporal_filter == MM_FILTER_IIR)
+        return MM_ERR_UNSUPPORTED;
     return do_compute_state(h, (const uint8_t *)in_dev, format, (c2 *)dev_buf, s);
 }
 

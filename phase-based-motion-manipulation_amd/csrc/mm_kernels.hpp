@@ -48,6 +48,11 @@ struct Spec {
     float hp_lo, hp_inv;    // high-pass ramp start maxF*0.8, 1/(maxF*0.2)
     float lp_hi, lp_inv;    // low-pass ramp end minF*1.2, 1/(minF*0.2)
     float lo[kMaxLevels], hi[kMaxLevels], inv_w[kMaxLevels];  // middle bands
+    // MM_MODE_STEERABLE (mm_steer.hpp): orientations, filter, IIR coefficients,
+    // orientation unit vectors (cos, sin of 2 pi k / O)
+    int O, filt;
+    float r_low, r_high;
+    float ang_c[8], ang_s[8];
 };
 
 struct Blur5 { float w0, w1, w2; };  // taps at 0, +-1, +-2 texels

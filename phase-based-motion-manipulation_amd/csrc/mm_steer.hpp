@@ -1,0 +1,244 @@
+// mm_steer.hpp — MM_MODE_STEERABLE (extension f2): oriented
+// local-phase subbands with a per-coefficient temporal filter.  Spec and CPU
+// oracle: oracle/steerable_ref.py (no reference counterpart; parity of the
+// shared stages is pinned by its S = 0 identity with the reference path).
+//
+// Per frame, after K1 (row FFTs -> G):
+//   k_cols_fwd : G columns -> F, the half spectrum (f <= N/2, all fy)
+//   k_sb_cols  : one column kx of F (Hermitian mirror for kx > N/2) times each
+//                band mask  m_i a_o / N^2  (o < O/2) and the residual mask
+//                (m_0 + m_{L-1}) / N^2 -> column IFFT -> T[band][kx][k] for
+//                the Hn list rows the crop + blur need
+//   k_sb_rows  : one list row k: per band the row IFFT -> local coefficient
+//                s(x); in the W+4 columns the blur reads, phase filter vs the
+//                state, s' = s e^{i S P} (gated |s| < tau), y += 2 Re s';
+//                residual y += Re s;  |y| -> horizontal 5-tap blur -> Yh
+// then K4 (k_compose) as in the other modes.
+#pragma once
+#include "mm_kernels.hpp"
+
+namespace mm {
+
+// GeneratePyramidFilters (PyramidOperations.compute:25-87) for level i at radius fr.
+__device__ __forceinline__ float level_mask(float fr, int i, const Spec &sp)
+{
+    if (i == 0)
+        return fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
+    if (i == sp.L - 1)
+        return fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+    return (fr >= sp.lo[i] && fr <= sp.hi[i])
+               ? 0.5f * (1.0f + __cosf(2.0f * kPi * ((fr - sp.lo[i]) * sp.inv_w[i] - 0.5f)))
+               : 0.0f;
+}
+
+__device__ __forceinline__ float pow4(float x) { x *= x; return x * x; }
+
+// normalize_phase (PyramidPhaseDifference.compute:47-54) for |x| < 3 pi
+__device__ __forceinline__ float wrap_pi(float x)
+{
+    if (x > kPi) x -= 2.0f * kPi;
+    if (x < -kPi) x += 2.0f * kPi;
+    return x;
+}
+
+// signed true frequency / N of index k: k < N/2 -> k, else k - N (N/2 -> -1/2)
+template <int N> __device__ __forceinline__ float sfreq(int k)
+{
+    return (float)(k < N / 2 ? k : k - N) * (1.0f / (float)N);
+}
+
+// -------------------------------------------------------------------------
+// F of every chunk frame: column FFTs of K1's G, stored as Fb[fr][f][fy].
+// -------------------------------------------------------------------------
+template <int LOG2N>
+__global__ __launch_bounds__(wg_threads<LOG2N>())
+void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, size_t f_stride,
+                int total_cols, Geo g, const c2 *__restrict__ tw)
+{
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int F = N / 2 + 1;
+    extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
+    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    c2 *lds = lds_all + grp * lds_complex<N>();
+    const int logical = blockIdx.x * GPW + grp;
+    const bool valid = logical < total_cols;
+    const int fr = valid ? logical / F : 0, f = valid ? logical % F : 0;
+    const c2 *Gc = G + (size_t)fr * g_stride + (size_t)f * g.H;
+    c2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int rr = t + j * T - g.y0;
+        const c2 a = Gc[min(max(rr, 0), g.H - 1)];
+        v[j] = (rr >= 0 && rr < g.H) ? a : mk(0.0f, 0.0f);
+    }
+    fft_regs<LOG2N, -1>(v, t, lds, tw);
+    if (valid) {
+        c2 *out = Fb + (size_t)fr * f_stride + (size_t)f * N;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) out[t + j * T] = v[j];
+    }
+}
+
+// -------------------------------------------------------------------------
+// Band columns: T[b][kx][k] = IFFT_col(F m_i a_o / N^2)[canvas row rb + k]
+// -------------------------------------------------------------------------
+template <int LOG2N>
+__global__ __launch_bounds__(wg_threads<LOG2N>())
+void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_stride, Geo g, Spec sp,
+               const c2 *__restrict__ tw)
+{
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
+    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    c2 *lds = lds_all + grp * lds_complex<N>();
+    const int kx_raw = blockIdx.x * GPW + grp;
+    const bool valid = kx_raw < N;               // small N: more groups than columns
+    const int kx = valid ? kx_raw : N - 1;
+    const bool mir = kx > N / 2;
+    const c2 *Fc = Fb + (size_t)(mir ? N - kx : kx) * N;
+    const float fxs = sfreq<N>(kx);
+    c2 v0[8];
+    float fr[8], cx[8], sy[8], isum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int ky = t0 + j * T;
+        c2 a = Fc[mir ? (N - ky) & (N - 1) : ky];     // F(-f) = conj F(f) (real input)
+        if (mir) a.y = -a.y;
+        v0[j] = scale(a, sp.inv_nn);
+        const float fys = sfreq<N>(ky);
+        const float r2 = fxs * fxs + fys * fys;
+        fr[j] = __builtin_amdgcn_sqrtf(r2);
+        const bool flat = kx == N / 2 || ky == N / 2 || r2 == 0.0f;   // a_o = 1/O
+        const float ir = flat ? 0.0f : 1.0f / fr[j];
+        cx[j] = fxs * ir;
+        sy[j] = fys * ir;
+        float sum = 0.0f;
+        for (int k = 0; k < sp.O; ++k) sum += pow4(fmaxf(0.0f, cx[j] * sp.ang_c[k] + sy[j] * sp.ang_s[k]));
+        isum[j] = flat ? -1.0f : 1.0f / sum;
+    }
+    const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
+    const int nb = nmid * (sp.O / 2);
+    for (int b = 0; b <= nb; ++b) {
+        // opaque lane index per band: keeps LICM from hoisting the FFT addressing
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        const int o = nmid ? b / nmid : 0, i = nmid ? 1 + b % nmid : 0;
+        c2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float m;
+            if (b == nb) {   // residual: levels 0 and L-1, no orientation
+                m = level_mask(fr[j], 0, sp) + (sp.L > 1 ? level_mask(fr[j], sp.L - 1, sp) : 0.0f);
+            } else {
+                const float ao = isum[j] < 0.0f
+                                     ? 1.0f / (float)sp.O
+                                     : pow4(fmaxf(0.0f, cx[j] * sp.ang_c[o] + sy[j] * sp.ang_s[o])) * isum[j];
+                m = level_mask(fr[j], i, sp) * ao;
+            }
+            v[j] = scale(v0[j], m);
+        }
+        fft_regs<LOG2N, +1>(v, t, lds, tw);
+        c2 *out = Tb + (size_t)b * band_stride + (size_t)kx * g.Hq;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
+            if (valid && k < g.Hn) out[k] = v[j];
+        }
+    }
+}
+
+// -------------------------------------------------------------------------
+// Band rows: local phase filter, amplification, synthesis, |.|, H blur -> Yh
+// -------------------------------------------------------------------------
+// State planes (floats): phi[b][k][xi], u_h[...], u_l[...] for the Wc = W+4
+// canvas columns x0-2 .. x0+W+1 the horizontal blur reads (xi = x - (x0-2)
+// mod N).  reset: first frame (phi <- arg s, u <- 0, nothing amplified).
+template <int LOG2N>
+__global__ __launch_bounds__(wg_threads<LOG2N>())
+void k_sb_rows(const c2 *__restrict__ Tb, size_t band_stride, float *__restrict__ Yh,
+               float *__restrict__ st_phi, float *__restrict__ st_uh, float *__restrict__ st_ul,
+               int reset, int write_out, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
+{
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
+    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    c2 *lds = lds_all + grp * lds_complex<N>();
+    const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
+    const bool valid = logical < g.Hn;
+    const int k = valid ? logical : g.Hn - 1;   // list row (canvas row rb + k)
+    const int Wc = g.W + 4, xs = g.x0 - 2;
+    const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
+    const int nb = nmid * (sp.O / 2);
+    float y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = 0.0f;
+    for (int b = 0; b <= nb; ++b) {
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        const c2 *col = Tb + (size_t)b * band_stride + k;
+        c2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = col[(size_t)(t + j * T) * g.Hq];
+        fft_regs<LOG2N, +1>(v, t, lds, tw);
+        if (b == nb) {   // residual: Hermitian, real output
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] += v[j].x;
+            continue;
+        }
+        const size_t row = ((size_t)b * g.Hn + k) * Wc;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int xi = (t + j * T - xs + N) & (N - 1);
+            if (valid && xi < Wc) {
+                const size_t si = row + xi;
+                const float ph = atan2f(v[j].y, v[j].x);
+                float P = 0.0f, uh = 0.0f, ul = 0.0f;
+                if (!reset) {
+                    const float pp = st_phi[si];
+                    if (sp.filt == MM_FILTER_DIFF) {
+                        P = wrap_pi(pp - ph);              // prev - cur, as the reference
+                    } else {
+                        const float d = wrap_pi(ph - pp);
+                        uh = (1.0f - sp.r_high) * (st_uh[si] + d);
+                        ul = (1.0f - sp.r_low) * (st_ul[si] + d);
+                        P = ul - uh;
+                    }
+                }
+                st_phi[si] = ph;
+                if (sp.filt == MM_FILTER_IIR) {
+                    st_uh[si] = uh;
+                    st_ul[si] = ul;
+                }
+                c2 s2 = v[j];
+                if (write_out && v[j].x * v[j].x + v[j].y * v[j].y >= sp.tau2) {
+                    const float a = sp.S * P;
+                    s2 = mul(v[j], mk(__cosf(a), __sinf(a)));
+                }
+                y[j] += 2.0f * s2.x;
+            }
+        }
+    }
+    if (!write_out) return;
+    // |y| (ConvertComplexMagToTex) then the horizontal half of ApplyAntiAliasing
+    float *raw = reinterpret_cast<float *>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[j]);
+    __syncthreads();
+    if (!valid) return;
+    float *out = Yh + (size_t)k * g.W;
+    const bool interior = g.x0 >= 2 && g.x0 + g.W + 2 <= N;
+    for (int X = t0; X < g.W; X += T) {
+        const int c = g.x0 + X;
+        float acc;
+        if (interior) {
+            acc = bw.w0 * raw[c] + bw.w1 * (raw[c - 1] + raw[c + 1]) + bw.w2 * (raw[c - 2] + raw[c + 2]);
+        } else {
+            acc = bw.w0 * raw[wrap_idx(c, N, g.edge)];
+            acc += bw.w1 * (raw[wrap_idx(c - 1, N, g.edge)] + raw[wrap_idx(c + 1, N, g.edge)]);
+            acc += bw.w2 * (raw[wrap_idx(c - 2, N, g.edge)] + raw[wrap_idx(c + 2, N, g.edge)]);
+        }
+        out[X] = acc;
+    }
+}
+
+}  // namespace mm

@@ -17,12 +17,14 @@ There is no CPU fallback.  If the library or a gfx950 device is missing,
 construction/Start raises ``MMError`` — loudly, never silently.
 """
 from .binding import (MMError, lib, load_library, LIB_PATH, RGBA8, RGBA32F,
-                      EDGE_REPEAT, EDGE_CLAMP, MODE_PYRAMID, MODE_STANDARD, Params, Handle,
+                      EDGE_REPEAT, EDGE_CLAMP, MODE_PYRAMID, MODE_STANDARD, MODE_STEERABLE,
+                      FILTER_DIFF, FILTER_IIR, Params, Handle,
                       abi_symbols, resample_table, strerror)
 from .processor import MotionMagnificationProcessor
 from .stream import ShardedStream, shard_range
 
 __all__ = ["MMError", "lib", "load_library", "LIB_PATH", "RGBA8", "RGBA32F",
-           "EDGE_REPEAT", "EDGE_CLAMP", "MODE_PYRAMID", "MODE_STANDARD", "Params", "Handle", "abi_symbols",
+           "EDGE_REPEAT", "EDGE_CLAMP", "MODE_PYRAMID", "MODE_STANDARD", "MODE_STEERABLE",
+           "FILTER_DIFF", "FILTER_IIR", "Params", "Handle", "abi_symbols",
            "resample_table", "strerror", "MotionMagnificationProcessor",
            "ShardedStream", "shard_range"]

@@ -16,6 +16,9 @@ EDGE_REPEAT = 0
 EDGE_CLAMP = 1
 MODE_PYRAMID = 0
 MODE_STANDARD = 1
+MODE_STEERABLE = 2      # extension f2 (oracle/steerable_ref.py)
+FILTER_DIFF = 0
+FILTER_IIR = 1
 FRAMES_ON_DEVICE = 1
 
 KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv", "k_compose")   # MM_K_* ids 0..3
@@ -42,7 +45,9 @@ class Params(ctypes.Structure):
                 ("high_frequency_cutoff", ctypes.c_float), ("filter_steepness", ctypes.c_float),
                 ("motion_sensitivity", ctypes.c_float), ("enhance_edges", ctypes.c_int),
                 ("edge_enhancement", ctypes.c_float),
-                ("show_magnitude", ctypes.c_int), ("show_phase", ctypes.c_int)]
+                ("show_magnitude", ctypes.c_int), ("show_phase", ctypes.c_int),
+                ("temporal_filter", ctypes.c_int), ("iir_low", ctypes.c_float),
+                ("iir_high", ctypes.c_float)]
 
     @classmethod
     def make(cls, levels=5, min_freq=0.05, max_freq=0.45, phase_scale=10.0,
@@ -51,7 +56,8 @@ class Params(ctypes.Structure):
         """other mm.h fields by keyword: the standard-mode band-pass
         (apply_bandpass_filter, low_frequency_cutoff, high_frequency_cutoff,
         filter_steepness, motion_sensitivity, enhance_edges, edge_enhancement)
-        and the debug views (show_magnitude, show_phase)."""
+        the debug views (show_magnitude, show_phase) and the steerable
+        extension (orientations, temporal_filter, iir_low, iir_high)."""
         p = cls()
         lib().mm_params_default(ctypes.byref(p))
         p.levels, p.min_freq, p.max_freq = levels, min_freq, max_freq
@@ -62,12 +68,13 @@ class Params(ctypes.Structure):
             if k not in dict(cls._fields_):
                 raise TypeError(f"unknown mm_params field {k}")
             setattr(p, k, int(v) if k in ("apply_bandpass_filter", "enhance_edges",
-                                          "show_magnitude", "show_phase") else v)
+                                          "show_magnitude", "show_phase", "orientations",
+                                          "temporal_filter") else v)
         return p
 
 
 _lib = None
-ABI_VERSION = 3   # include/mm.h MM_ABI_VERSION
+ABI_VERSION = 4   # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):

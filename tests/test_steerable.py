@@ -1,0 +1,150 @@
+"""MM_MODE_STEERABLE (extension f2): the spec oracle's
+identities on CPU, and the HIP path against the spec on the GPU.
+
+Parity against the reference is unpinned (no reference implementation exists,
+oracle/steerable_ref.py); what is pinned: at S = 0 the whole chain equals the
+reference pipeline (C oracle) exactly up to rounding, and the HIP path equals
+the float64 spec at every S within the tolerances below.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import mmtest as T
+import np_twin
+import oracle_py as O
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import steerable_ref as SR  # noqa: E402
+
+
+def frames(W, H, n):
+    return [O.synth_frame(W, H, t).astype(np.float32) / np.float32(255) for t in range(n)]
+
+
+# ---- spec identities (CPU) ----------------------------------------------------
+
+@pytest.mark.parametrize("Oo", [4, 6, 8])
+def test_angular_partition_and_mirror(Oo):
+    N = 64
+    a = SR.angular_masks(N, Oo)
+    assert np.abs(a.sum(0) - 1).max() < 1e-12
+    idx = (N - np.arange(N)) % N
+    for o in range(Oo):
+        assert np.abs(a[o][np.ix_(idx, idx)] - a[(o + Oo // 2) % Oo]).max() < 1e-12
+
+
+@pytest.mark.parametrize("filt", [SR.FILTER_DIFF, SR.FILTER_IIR])
+def test_spec_s0_is_reference_pipeline(filt):
+    W, H = 64, 48
+    fr = [f.astype(np.float64) for f in frames(W, H, 3)]
+    r = SR.SteerableRef(W, H, levels=5, phase_scale=0.0, orientations=8, filt=filt)
+    outs = [r.process(f) for f in fr]
+    assert np.array_equal(outs[0], fr[0])
+    ref = np_twin.process_frame(fr[2], fr[1], 5, 0.05, 0.45, 0.0)
+    assert np.abs(outs[2] - ref).max() < 1e-12
+
+
+def test_spec_static_scene_unchanged_by_diff():
+    """DIFF on a static scene: P = 0 everywhere, output = S=0 output."""
+    W, H = 64, 48
+    f = frames(W, H, 1)[0].astype(np.float64)
+    a = SR.SteerableRef(W, H, phase_scale=25.0, orientations=4)
+    b = SR.SteerableRef(W, H, phase_scale=0.0, orientations=4)
+    for _ in range(3):
+        oa, ob = a.process(f), b.process(f)
+    assert np.abs(oa - ob).max() < 1e-12
+
+
+# ---- HIP path (GPU) -------------------------------------------------------------
+
+def gpu_steer(W, H, fr, levels=5, S=10.0, Oo=8, filt=0, rl=0.05, rh=0.4, edge=0, apply=True):
+    import mm355
+    import torch
+    p = mm355.Params.make(levels=levels, phase_scale=S, edge_mode=edge, apply_magnification=apply,
+                          mode=mm355.MODE_STEERABLE, orientations=Oo, temporal_filter=filt,
+                          iir_low=rl, iir_high=rh)
+    h = mm355.Handle(W, H, p)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    out = torch.empty_like(dev)
+    h.process_stream(dev, out, len(fr), mm355.RGBA32F)
+    torch.cuda.synchronize()
+    res = out.cpu().numpy()
+    h.close()
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Oo,filt", [(8, 0), (4, 1)])
+def test_gpu_s0_equals_reference_oracle(Oo, filt):
+    W, H = 96, 64
+    fr = frames(W, H, 4)
+    got = gpu_steer(W, H, fr, S=0.0, Oo=Oo, filt=filt)
+    ref = T.oracle_run(W, H, fr, levels=5, S=0.0)
+    assert np.array_equal(got[0], fr[0])
+    T.assert_close_f32(got[1:], np.stack(ref[1:]))
+
+
+def _close_spec(got, ref):
+    """fp32 HIP vs float64 spec: amplified local phase S*P (P wraps at +-pi
+    where the two sides may fall differently): 99.9th percentile <= 2e-4,
+    RMSE <= 2e-5."""
+    e = np.abs(got.astype(np.float64) - ref)
+    assert np.quantile(e, 0.999) < 2e-4 and np.sqrt((e ** 2).mean()) < 2e-5, (
+        e.max(), np.quantile(e, 0.999), np.sqrt((e ** 2).mean()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,Oo,filt,S,edge", [(64, 48, 8, 0, 10.0, 0), (96, 64, 4, 1, 25.0, 0),
+                                                 (64, 48, 6, 1, 9.7, 1), (200, 120, 8, 0, 25.0, 0)])
+def test_gpu_matches_spec(W, H, Oo, filt, S, edge):
+    n = 5
+    fr = frames(W, H, n)
+    got = gpu_steer(W, H, fr, S=S, Oo=Oo, filt=filt, edge=edge)
+    r = SR.SteerableRef(W, H, levels=5, phase_scale=S, orientations=Oo, filt=filt, edge=edge)
+    ref = [r.process(f.astype(np.float64)) for f in fr]
+    assert np.array_equal(got[0], fr[0])
+    for k in range(1, n):
+        _close_spec(got[k], ref[k])
+
+
+@pytest.mark.gpu
+def test_gpu_chunked_and_state_handoff():
+    """Chunk boundaries (MM_CHUNK 8 by default) and the DIFF state hand-off:
+    a second handle seeded with mm_compute_state(frame k-1) continues the
+    stream bitwise; mm_get_state/mm_set_state carry the IIR state."""
+    import mm355
+    import torch
+    W, H, n = 64, 48, 11
+    fr = frames(W, H, n)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    for filt in (0, 1):
+        p = mm355.Params.make(levels=5, phase_scale=10.0, mode=mm355.MODE_STEERABLE,
+                              orientations=8, temporal_filter=filt)
+        a = mm355.Handle(W, H, p)
+        full = torch.empty_like(dev)
+        a.process_stream(dev, full, n, mm355.RGBA32F)
+        b = mm355.Handle(W, H, p)
+        part = torch.empty_like(dev)
+        b.process_stream(dev[:6], part[:6], 6, mm355.RGBA32F)
+        st = torch.empty(b.state_bytes, dtype=torch.uint8, device="cuda")
+        b.get_state(st)
+        c = mm355.Handle(W, H, p)
+        c.set_state(st)
+        c.process_stream(dev[6:], part[6:], n - 6, mm355.RGBA32F)
+        torch.cuda.synchronize()
+        assert torch.equal(full, part), filt
+        if filt == 0:
+            d = mm355.Handle(W, H, p)
+            st2 = torch.empty(d.state_bytes, dtype=torch.uint8, device="cuda")
+            d.compute_state(dev[5], mm355.RGBA32F, st2)
+            d.set_state(st2)
+            o = torch.empty_like(dev[6:])
+            d.process_stream(dev[6:], o, n - 6, mm355.RGBA32F)
+            torch.cuda.synchronize()
+            assert torch.equal(o, full[6:])
+            d.close()
+        for h in (a, b, c):
+            h.close()
