@@ -741,6 +741,7 @@ void mm_ref_process_u8(mm_ref *c, const uint8_t *in, uint8_t *out)
     const size_t px = (size_t)c->W * c->H * 4;
     float *fi = (float *)malloc(sizeof(float) * px);
     float *fo = (float *)malloc(sizeof(float) * px);
+    if (!fi || !fo) { free(fi); free(fo); return; }
     int passthrough = c->first || (!c->apply && !c->show_mag && !c->show_phase);
     for (size_t i = 0; i < px; ++i) fi[i] = (float)in[i] / 255.0f;
     mm_ref_process(c, fi, fo, NULL);
