@@ -282,7 +282,7 @@ template <int LOG2N>
 static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 *st_in,
                      c2 *st_out, hipStream_t s)
 {
-    const int gpw = groups_per_wg<LOG2N>();
+    const int gpw = k2_groups<LOG2N>();
     const int cols = (1 << LOG2N) / 2;   // f = 0 and f = N/2 share group 0 (k_cols)
     const int blocks = (cols + gpw - 1) / gpw;
     ProfScope ps(h, s, MM_K_COLS, nframes);
@@ -305,7 +305,7 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     // per group: FFT exchange buffer + two per-bin tables (k_cols)
     const size_t lds = k2_lds_bytes<LOG2N>();
 #define MM_K2_LAUNCH(MODE)                                                                 \
-    hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(wg_threads<LOG2N>()), lds, s, \
+    hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, \
                        h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,       \
                        first_passthrough, h->geo, h->spec, h->d_tw)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
@@ -753,6 +753,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.rb = g.y0 - 2;
     g.Hn = std::min(height + 4, N);
     g.Hq = (g.Hn + 1) & ~1;
+    g.Qs = N / 2 + 2;
     g.edge = p->edge_mode;
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
@@ -767,7 +768,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     const char *k2 = getenv("MM_K2");
     h->k2_wave = k2 && strcmp(k2, "wave") == 0;
     h->g_stride = (size_t)(N / 2 + 1) * height;
-    h->q_stride = (size_t)(N / 2 + 1) * g.Hq;
+    h->q_stride = (size_t)g.Qs * g.Hq;
     h->yh_stride = (size_t)g.Hn * width;
 
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -4,9 +4,9 @@
 //   K1 k_rows_fwd : RGBA frame --(luma, stretch+pad bilinear, Hann window)-->
 //                   real rows --(paired real FFT)--> G[f][row]       (f < F)
 //   K2 k_cols     : G column --FFT--> F_t --(pyramid phase op vs F_{t-1})-->
-//                   A --IFFT--> Q[f][row]; F_t becomes the state.  One WG owns
-//                   a column for a whole chunk of frames, so F_{t-1} stays in
-//                   registers between frames.
+//                   A --IFFT--> Q[row/2][f][row%2]; F_t becomes the state.
+//                   One FFT group owns a column for a whole chunk of frames, so
+//                   F_{t-1} stays in registers between frames.
 //   K3 k_rows_inv : Q rows --(paired C2R IFFT)--> |z| --(5-tap H blur)--> Yh
 //   K4 k_compose  : Yh --(5-tap V blur)--, input --(I/Q resample)--> YIQ->RGB,
 //                   saturate, crop --> RGBA frame
@@ -33,7 +33,8 @@ struct Geo {
     int x0, y0;       // image placement inside the canvas (PadTexture .cs:360-363)
     int rb;           // canvas row of Q list index 0 (= y0 - 2)
     int Hn;           // rows kept in Q (= min(H + 4, N))
-    int Hq;           // Q column stride (Hn rounded to even)
+    int Hq;           // Hn rounded to even (row-pair count of Q = Hq / 2)
+    int Qs;           // Q pair-row stride in bins (N/2 + 2; q_index)
     int edge;         // 0 repeat, 1 clamp
 };
 
@@ -95,6 +96,13 @@ template <class T>
 __device__ __forceinline__ void st_off(void *base, unsigned byte_off, T v)
 {
     *reinterpret_cast<T *>(reinterpret_cast<uint8_t *>(base) + byte_off) = v;
+}
+
+// Q hand-off (K2 -> K3): element (row k, bin f) of a frame, stored by row pairs
+// [k/2][f][k%2], pair-row stride Qs bins (float4 (row 2m, row 2m+1) per bin)
+__device__ __forceinline__ size_t q_index(const Geo &g, int k, int f)
+{
+    return ((size_t)(k >> 1) * g.Qs + f) * 2 + (k & 1);
 }
 
 // ---- pixel access -------------------------------------------------------
@@ -476,11 +484,17 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
 }
 
 template <int LOG2N> constexpr int k2_tab_entries() { return (1 << LOG2N) / 2 + 1; }
-// dynamic LDS of k_cols: per group the FFT exchange buffer and two tables
+// k_cols runs at least two columns per workgroup, so that a Q row receives one
+// 16-B (or wider) piece per workgroup instead of one 8-B value per column
+template <int LOG2N> constexpr int k2_groups() { return groups_per_wg<LOG2N>() < 2 ? 2 : groups_per_wg<LOG2N>(); }
+template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * fft_T<LOG2N>(); }
+// dynamic LDS of k_cols: per group the FFT exchange buffer and its column's
+// per-bin table, plus one table for column N/2 (packed group only)
 template <int LOG2N> constexpr size_t k2_lds_bytes()
 {
-    return (size_t)groups_per_wg<LOG2N>() *
-           (sizeof(c2) * lds_complex<(1 << LOG2N)>() + 2 * sizeof(float2) * k2_tab_entries<LOG2N>());
+    return (size_t)k2_groups<LOG2N>() *
+               (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_entries<LOG2N>()) +
+           sizeof(float2) * k2_tab_entries<LOG2N>();
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
@@ -493,22 +507,27 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 // WGs/CU instead of 1025 with a one-WG tail).  Column N/2's F_{t-1} lives in the
 // state buffer between frames.
 template <int LOG2N, int MODE>
-__global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_t q_stride,
             const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
             Geo g, Spec sp, const c2 *__restrict__ tw)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     constexpr int TE = k2_tab_entries<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    // group index: wave-uniform (scalar) when a group spans whole waves
+    const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
+    const int t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
-    float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * 2 * TE;
-    float2 *tabN = tab0 + TE;
-    const int f_raw = blockIdx.x * GPW + grp;
+    float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TE;
+    float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TE;
+    // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
+    // are merged in one L2 (split over XCDs they left as partial-line writes)
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
-    const bool blk0 = blockIdx.x == 0;        // uniform: block 0 runs the extra exchanges
+    const bool blk0 = blk == 0;               // uniform: block 0 runs the extra exchanges
     const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
     c2 *stN = state_out + (size_t)(N / 2) * N;
 
@@ -609,22 +628,37 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
             __builtin_amdgcn_sched_barrier(0);
         }
         fft_regs<LOG2N, +1>(v, t, lds, tw);
-        if (valid) {
-            c2 *Qc = Q + (size_t)fr * q_stride + (size_t)f * g.Hq;
-            c2 *QN = Q + (size_t)fr * q_stride + (size_t)(N / 2) * g.Hq;
+        // Q is stored by row pairs (q_index) so that K3 reads each of its two
+        // rows' values as one 16-B piece per bin, contiguous across the wave (a
+        // column-major Q made K3's 16-B gathers cost it 4 of its 7 us/frame at
+        // 1080p).  The GPW columns of the workgroup are transposed through LDS
+        // (over the exchange buffers: every group has passed the barrier after
+        // its last exchange read) and leave as one contiguous GPW*16-byte piece
+        // per row pair; same-XCD workgroups complete the 128-B lines.
+        c2 *Qf = Q + (size_t)fr * q_stride;
+        c2 *stg = lds_all;   // [Hq/2][GPW][2]
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-                if (k < g.Hn) {
-                    if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
-                        Qc[k] = mk(v[j].x, 0.0f);
-                        QN[k] = mk(v[j].y, 0.0f);
-                    } else {
-                        Qc[k] = v[j];
-                    }
+        for (int j = 0; j < 8; ++j) {
+            const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
+            if (valid && k < g.Hq) {
+                const int s = ((k >> 1) * GPW) * 2 + (k & 1);
+                if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
+                    stg[s] = mk(v[j].x, 0.0f);
+                    Qf[q_index(g, k, N / 2)] = mk(v[j].y, 0.0f);
+                } else {
+                    stg[s + 2 * grp] = v[j];
                 }
             }
         }
+        __syncthreads();
+        const int fb = blk * GPW;
+        for (int e = threadIdx.x; e < (g.Hq >> 1) * GPW; e += GPW * T) {
+            const int kp = e / GPW, c = e - kp * GPW;
+            if (GPW <= N / 2 || fb + c < N / 2)   // tiny N: fewer columns than groups
+                st_off<float4>(Qf, (unsigned)(kp * g.Qs + fb + c) * 16u,
+                               reinterpret_cast<const float4 *>(stg)[e]);
+        }
+        __syncthreads();   // the next frame's FFT rewrites the buffers
     }
     if (valid) {
         if (packed) {
@@ -671,13 +705,15 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
     const bool valid = logical < total_pairs;
     const int frame = frame0 + (valid ? logical / pairs_per_frame : 0);
     const int ka = valid ? 2 * (logical % pairs_per_frame) : 0;
-    const c2 *Qf = Q + (size_t)frame * q_stride + ka;
+    // row pair (ka, ka+1) of Q (q_index): one 16-B piece per bin, contiguous
+    const float4 *Qp = reinterpret_cast<const float4 *>(Q + (size_t)frame * q_stride) +
+                       (size_t)(ka >> 1) * g.Qs;
     float4 qv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {   // all 8 loads in flight (addresses always valid)
         const int fq = t + j * T;
         const int ff = fq > N / 2 ? N - fq : fq;
-        qv[j] = *reinterpret_cast<const float4 *>(Qf + (size_t)ff * g.Hq);
+        qv[j] = Qp[ff];
     }
     c2 v[8];
 #pragma unroll
@@ -700,6 +736,23 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
     __syncthreads();
     if (!valid) return;
     float *out = Yh + (size_t)frame * yh_stride + (size_t)ka * g.W;
+    if (g.x0 >= 4 && g.x0 % 4 == 0 && g.W % 4 == 0 && g.x0 + g.W + 4 <= N) {
+        // four outputs per thread from three aligned ds_read_b128 (taps c-2..c+5),
+        // one 16-B store; same expression and order as the scalar form below
+        const int W4 = g.W / 4;
+        for (int e = t; e < 2 * W4; e += T) {
+            const int r = e >= W4 ? 1 : 0, X = 4 * (e - r * W4);
+            const float4 *rw = reinterpret_cast<const float4 *>(raw + r * N + g.x0 + X);
+            const float4 A = rw[-1], B = rw[0], C = rw[1];
+            float4 o;
+            o.x = bw.w0 * B.x + bw.w1 * (A.w + B.y) + bw.w2 * (A.z + B.z);
+            o.y = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
+            o.z = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
+            o.w = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
+            *reinterpret_cast<float4 *>(out + (size_t)r * g.W + X) = o;
+        }
+        return;
+    }
     const bool interior = g.x0 >= 2 && g.x0 + g.W + 2 <= N;
     for (int e = t; e < 2 * g.W; e += T) {
         const int r = e >= g.W ? 1 : 0, X = e - r * g.W;

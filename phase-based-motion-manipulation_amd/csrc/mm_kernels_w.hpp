@@ -126,11 +126,11 @@ __device__ __forceinline__ void cols_plain(const c2 *__restrict__ G, size_t g_st
         }
         __builtin_amdgcn_sched_barrier(0);
         wf::fft<LOG2N, +1, E>(v, lane, buf, tw);
-        c2 *Qc = Q + (size_t)fr * q_stride + (size_t)f * g.Hq;
+        c2 *Qc = Q + (size_t)fr * q_stride;   // pair-interleaved Q (q_index)
 #pragma unroll
         for (int m = 0; m < P; ++m) {
             const int k = (lane + 64 * m - g.rb + 2 * N) & (N - 1);
-            if (k < g.Hn) Qc[k] = v[m];
+            if (k < g.Hn) Qc[q_index(g, k, f)] = v[m];
         }
     }
     if (last) {
@@ -220,14 +220,13 @@ __device__ __forceinline__ void cols_packed(const c2 *__restrict__ G, size_t g_s
         }
         wf::wave_sync();
         wf::fft<LOG2N, +1, E>(v, lane, buf, tw);
-        c2 *Qc = Q + (size_t)fr * q_stride;
-        c2 *QN = Q + (size_t)fr * q_stride + (size_t)(N / 2) * g.Hq;
+        c2 *Qc = Q + (size_t)fr * q_stride;   // pair-interleaved Q (q_index)
 #pragma unroll
         for (int m = 0; m < P; ++m) {   // inverse of A0 + i AN: real parts Q0 + i QN
             const int k = (lane + 64 * m - g.rb + 2 * N) & (N - 1);
             if (k < g.Hn) {
-                Qc[k] = mk(v[m].x, 0.0f);
-                QN[k] = mk(v[m].y, 0.0f);
+                Qc[q_index(g, k, 0)] = mk(v[m].x, 0.0f);
+                Qc[q_index(g, k, N / 2)] = mk(v[m].y, 0.0f);
             }
         }
     }
