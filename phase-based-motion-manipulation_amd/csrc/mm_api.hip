@@ -246,6 +246,13 @@ static int validate_params(const mm_params *p)
 // ------------------------------------------------------------------------
 // launches
 // ------------------------------------------------------------------------
+static int ilog2(int n)
+{
+    int l = 0;
+    while ((1 << l) < n) ++l;
+    return l;
+}
+
 template <int LOG2N> static size_t lds_fft_bytes()
 {
     return sizeof(c2) * (size_t)groups_per_wg<LOG2N>() * lds_complex<(1 << LOG2N)>();
@@ -262,17 +269,18 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
 {
     const int ppf = h->H / 2;
     const int total = ppf * nframes;
-    const int gpw = groups_per_wg<LOG2N>();
+    const int gpw = k1_groups<LOG2N>();
     const int blocks = (total + gpw - 1) / gpw;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t lds = sizeof(c2) * (size_t)gpw * lds_complex<(1 << LOG2N)>();
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
     if (fmt == MM_RGBA8)
-        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(k1_threads<LOG2N>()),
+                           lds, s, in, fb, ppf, total, h->geo, h->d_col3,
                            h->d_row3, h->d_tw, h->d_G, h->g_stride);
     else
-        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(wg_threads<LOG2N>()),
-                           lds_fft_bytes<LOG2N>(), s, in, fb, ppf, total, h->geo, h->d_col3,
+        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(k1_threads<LOG2N>()),
+                           lds, s, in, fb, ppf, total, h->geo, h->d_col3,
                            h->d_row3, h->d_tw, h->d_G, h->g_stride);
     HIPCHK(hipGetLastError());
     return MM_OK;
@@ -325,13 +333,14 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
 {
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
-    const int ppf = h->geo.Hn / 2;
+    const int ppf = h->geo.Hq / 2;   // whole Q tiles (k_rows_inv)
     const int total = ppf * nout;
-    const int gpw = groups_per_wg<LOG2N>();
+    const int gpw = k3_groups<LOG2N>();
     {
         ProfScope ps(h, s, MM_K_ROWS_INV, nout);
         hipLaunchKernelGGL((k_rows_inv<LOG2N>), dim3((total + gpw - 1) / gpw),
-                           dim3(wg_threads<LOG2N>()), lds_fft_bytes<LOG2N>(), s, h->d_Q,
+                           dim3(k3_threads<LOG2N>()), sizeof(c2) * (size_t)gpw * lds_complex<(1 << LOG2N)>(),
+                           s, h->d_Q,
                            h->q_stride, h->d_Yh, h->yh_stride, frame0, ppf, total, h->geo,
                            h->blur, h->d_tw);
         HIPCHK(hipGetLastError());
@@ -752,7 +761,8 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.y0 = (N - height) / 2;
     g.rb = g.y0 - 2;
     g.Hn = std::min(height + 4, N);
-    g.Hq = (g.Hn + 1) & ~1;
+    g.TK = q_tile_v(ilog2(N));
+    g.Hq = (g.Hn + g.TK - 1) / g.TK * g.TK;
     g.Qs = N / 2 + 2;
     g.edge = p->edge_mode;
     build_spec(*p, N, h->spec);

@@ -171,6 +171,21 @@ __device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *
     }
 }
 
+// LDS layout of the exchange after pass P: index i lives at
+// xpad(i) = i + A*(i >> S), chosen per pass (tools/lds_banks.py models the
+// gfx950 bank rules: ds_write_b64 in 4 groups of 16 lanes over 32 banks,
+// ds_read_b64 in 2 groups of 32 lanes over 64 banks).  Ns = 1 (8b + m
+// writes): pad8, the only linear form without write conflicts (its reads
+// stay 2-way on a few lanes); Ns = 8: A = 4, S = 5, conflict-free both ways;
+// Ns >= 64: none needed.  Against pad8 on every pass: 1.11x instead of
+// 1.56x the conflict-free LDS cycles at N = 512..4096.  Every layout fits
+// N + N/8 entries (lds_complex), and xpad(base + off) = xpad(base) +
+// xpad(off) for the offsets used, so LDS offsets stay immediates.
+constexpr int xpad_s(int log2n, int ns) { return log2n < 9 || ns == 1 ? 3 : (ns == 8 ? 5 : 30); }
+constexpr int xpad_a(int log2n, int ns) { return log2n < 9 || ns == 1 ? 1 : (ns == 8 ? 4 : 0); }
+template <int LOG2N, int NS>
+__host__ __device__ constexpr int xpad(int i) { return i + xpad_a(LOG2N, NS) * (i >> xpad_s(LOG2N, NS)); }
+
 // One Stockham pass (radix R, stride Ns).  B = 8/R butterflies per thread;
 // butterfly b = t + q*T reads x[b + m*N/R] (= register q + m*B) and writes
 // y[(b/Ns)*Ns*R + b%Ns + m*Ns].
@@ -194,23 +209,21 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
 #pragma unroll
             for (int m = 0; m < R; ++m) v[q + m * B] = u[m];
         } else {
-            // pad8(base + m Ns) = pad8(base) + m (Ns + Ns/8) for Ns >= 8, and
-            // pad8(base) + m for Ns = 1 (base = 8b): immediate LDS offsets
-            constexpr int step = NS == 1 ? 1 : NS + NS / 8;
-            c2 *row = lds + pad8((b / NS) * NS * R + (b & (NS - 1)));
+            // xpad(base + m Ns) = xpad(base) + xpad(m Ns): immediate LDS offsets
+            c2 *row = lds + xpad<LOG2N, NS>((b / NS) * NS * R + (b & (NS - 1)));
 #pragma unroll
-            for (int m = 0; m < R; ++m) row[m * step] = u[m];
+            for (int m = 0; m < R; ++m) row[xpad<LOG2N, NS>(m * NS)] = u[m];
         }
     }
     if constexpr (!LAST) {
         __syncthreads();
-        if constexpr (T % 8 == 0) {   // pad8(t + j T) = pad8(t) + j (T + T/8)
-            const c2 *col = lds + pad8(t);
+        if constexpr (T % 32 == 0) {   // xpad(t + j T) = xpad(t) + xpad(j T)
+            const c2 *col = lds + xpad<LOG2N, NS>(t);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = col[j * (T + T / 8)];
+            for (int j = 0; j < 8; ++j) v[j] = col[xpad<LOG2N, NS>(j * T)];
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = lds[pad8(t + j * T)];
+            for (int j = 0; j < 8; ++j) v[j] = lds[xpad<LOG2N, NS>(t + j * T)];
         }
         __syncthreads();
     }
@@ -234,6 +247,28 @@ __device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *_
     c2 wb[16];
     preload_twiddles<LOG2N, DIR>(wb, t, tw);
     fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wb);
+}
+
+// Slot i = P*4 + q of the twiddle-base array is used by pass P's butterfly q.
+constexpr bool tw_slot_used(int log2n, int i)
+{
+    return i / 4 >= 1 && i / 4 < fft_passes_v(log2n) && i % 4 < 8 / pass_radix_v(log2n, i / 4);
+}
+
+// Same, with the forward-direction twiddle bases already in registers
+// (preload_twiddles<LOG2N, -1>; the inverse uses their conjugates): for loops
+// that must not issue loads between frames.
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void fft_regs_w(c2 (&v)[8], int t, c2 *lds, const c2 (&wf)[16])
+{
+    if constexpr (DIR < 0) {
+        fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wf);
+    } else {
+        c2 wb[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wb[i] = mk(wf[i].x, -wf[i].y);
+        fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wb);
+    }
 }
 
 }  // namespace mm

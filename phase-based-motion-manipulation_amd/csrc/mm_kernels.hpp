@@ -33,8 +33,9 @@ struct Geo {
     int x0, y0;       // image placement inside the canvas (PadTexture .cs:360-363)
     int rb;           // canvas row of Q list index 0 (= y0 - 2)
     int Hn;           // rows kept in Q (= min(H + 4, N))
-    int Hq;           // Hn rounded to even (row-pair count of Q = Hq / 2)
-    int Qs;           // Q pair-row stride in bins (N/2 + 2; q_index)
+    int Hq;           // Hn rounded up to whole Q tiles (TK rows)
+    int Qs;           // Q bins per tile row (N/2 + 2; q_index)
+    int TK;           // rows per Q tile (q_tile_v)
     int edge;         // 0 repeat, 1 clamp
 };
 
@@ -61,6 +62,33 @@ struct Blur5 { float w0, w1, w2; };  // taps at 0, +-1, +-2 texels
 template <int LOG2N> constexpr int fft_T() { return (1 << LOG2N) / 8; }
 template <int LOG2N> constexpr int groups_per_wg() { return fft_T<LOG2N>() >= 256 ? 1 : 256 / fft_T<LOG2N>(); }
 template <int LOG2N> constexpr int wg_threads() { return groups_per_wg<LOG2N>() * fft_T<LOG2N>(); }
+// at least MIN FFT groups per workgroup (within 1024 threads)
+constexpr int groups_at_least_v(int log2n, int min)
+{
+    const int T = (1 << log2n) / 8, base = T >= 256 ? 1 : 256 / T;
+    if (base >= min) return base;
+    int g = min;
+    while (g > base && T * g > 1024) g /= 2;
+    return g;
+}
+template <int LOG2N, int MIN> constexpr int groups_at_least() { return groups_at_least_v(LOG2N, MIN); }
+#ifndef MM_K1_GROUPS
+#define MM_K1_GROUPS 2
+#endif
+#ifndef MM_K2_GROUPS
+#define MM_K2_GROUPS 2
+#endif
+#ifndef MM_K3_GROUPS
+#define MM_K3_GROUPS 4
+#endif
+// K3 runs one Q tile (TK = 2 * groups rows) per workgroup
+template <int LOG2N> constexpr int k3_groups() { return groups_at_least<LOG2N, MM_K3_GROUPS>(); }
+template <int LOG2N> constexpr int k3_threads() { return k3_groups<LOG2N>() * fft_T<LOG2N>(); }
+constexpr int q_tile_v(int log2n) { return 2 * groups_at_least_v(log2n, MM_K3_GROUPS); }
+template <int LOG2N> constexpr int q_tile() { return q_tile_v(LOG2N); }
+// K1 runs >= 2 row pairs per workgroup so that G receives 32-B pieces
+template <int LOG2N> constexpr int k1_groups() { return groups_at_least<LOG2N, MM_K1_GROUPS>(); }
+template <int LOG2N> constexpr int k1_threads() { return k1_groups<LOG2N>() * fft_T<LOG2N>(); }
 
 __device__ __forceinline__ int wrap_idx(int i, int n, int edge)
 {
@@ -98,11 +126,13 @@ __device__ __forceinline__ void st_off(void *base, unsigned byte_off, T v)
     *reinterpret_cast<T *>(reinterpret_cast<uint8_t *>(base) + byte_off) = v;
 }
 
-// Q hand-off (K2 -> K3): element (row k, bin f) of a frame, stored by row pairs
-// [k/2][f][k%2], pair-row stride Qs bins (float4 (row 2m, row 2m+1) per bin)
+// Q hand-off (K2 -> K3): element (row k, bin f) of a frame, stored in tiles of
+// TK rows: [k/TK][f][k%TK], Qs bins per tile row.  A K2 workgroup's columns of
+// one tile are contiguous (GPW*TK*8 bytes: whole 128-B lines at TK = 8), and
+// K3's TK/2 row pairs of a bin are one contiguous TK*8-byte block.
 __device__ __forceinline__ size_t q_index(const Geo &g, int k, int f)
 {
-    return ((size_t)(k >> 1) * g.Qs + f) * 2 + (k & 1);
+    return ((size_t)(k / g.TK) * g.Qs + f) * g.TK + (k % g.TK);
 }
 
 // ---- pixel access -------------------------------------------------------
@@ -181,17 +211,21 @@ __device__ __forceinline__ float2 chroma_iq(typename Pix<FMT>::raw_t u)
 // K1: luma rows -> half spectra of row pairs
 // =========================================================================
 template <int LOG2N, int FMT>
-__global__ __launch_bounds__(wg_threads<LOG2N>())
+__global__ __launch_bounds__(k1_threads<LOG2N>())
 void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pairs_per_frame,
                 int total_pairs, Geo g, const float4 *__restrict__ colW3,
                 const float4 *__restrict__ rowW3, const c2 *__restrict__ tw,
                 c2 *__restrict__ G, size_t g_stride)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k1_groups<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    // group index: wave-uniform (scalar) when a group spans whole waves
+    const int grp = GPW == 1 ? 0 : (T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T)
+                                               : threadIdx.x / T);
+    const int t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
-    const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
+    const int lblk = xcd_remap(blockIdx.x, gridDim.x) * GPW;   // block's first pair
+    const int logical = lblk + grp;
     const bool valid = logical < total_pairs;
     const int frame = valid ? logical / pairs_per_frame : 0;
     const int ra = valid ? 2 * (logical % pairs_per_frame) : 0;  // image row of pair
@@ -255,9 +289,8 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
 #pragma unroll
     for (int j = 0; j < 8; ++j) lds[pad8(t + j * T)] = v[j];
     __syncthreads();
-    if (!valid) return;
-    c2 *Gf = G + (size_t)frame * g_stride;
-    auto split_store = [&](int f) {
+    // half spectra of rows (ra, ra+1) at bins f = t + jT (j < 4) and N/2 (j = 4)
+    auto split = [&](int f) {
         c2 zf = lds[pad8(f)], zm = lds[pad8((N - f) & (N - 1))];
         // Y_a = (Z[f] + conj Z[N-f]) / 2 ;  Y_b = (Z[f] - conj Z[N-f]) / 2i
         float4 o;
@@ -265,11 +298,37 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         o.y = 0.5f * (zf.y - zm.y);
         o.z = 0.5f * (zf.y + zm.y);
         o.w = -0.5f * (zf.x - zm.x);
-        st_off<float4>(Gf, (unsigned)(f * g.H + ra) * 8u, o);
+        return o;
     };
+    float4 o[5];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) split_store(t + j * T);
-    if (t == 0) split_store(N / 2);
+    for (int j = 0; j < 4; ++j) o[j] = split(t + j * T);
+    o[4] = split(N / 2);
+    // G[f][row] is row-contiguous per bin.  With whole row-pair groups per
+    // frame in the workgroup (uniform test), the GPW pairs' values of a bin are
+    // transposed through LDS and leave as one 16*GPW-byte piece (consecutive
+    // rows); else every group stores its own 16-B pieces.
+    if (GPW == 1 || pairs_per_frame % GPW != 0) {
+        if (!valid) return;
+        c2 *Gf = G + (size_t)frame * g_stride;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st_off<float4>(Gf, (unsigned)((t + j * T) * g.H + ra) * 8u, o[j]);
+        if (t == 0) st_off<float4>(Gf, (unsigned)((N / 2) * g.H + ra) * 8u, o[4]);
+        return;
+    }
+    __syncthreads();   // split reads done before the staging overwrites the buffers
+    float4 *stg = reinterpret_cast<float4 *>(lds_all);   // [N/2 + 1][GPW]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stg[(t + j * T) * GPW + grp] = o[j];
+    if (t == 0) stg[(N / 2) * GPW + grp] = o[4];
+    __syncthreads();
+    if (lblk >= total_pairs) return;   // whole block past the end (total % GPW == 0)
+    const int fr0 = lblk / pairs_per_frame, ra0 = 2 * (lblk % pairs_per_frame);
+    c2 *Gf = G + (size_t)fr0 * g_stride;
+    for (int e = threadIdx.x; e < (N / 2 + 1) * GPW; e += GPW * T) {
+        const int f = e / GPW, c = e - f * GPW;
+        st_off<float4>(Gf, (unsigned)(f * g.H + ra0 + 2 * c) * 8u, stg[e]);
+    }
 }
 
 // =========================================================================
@@ -486,7 +545,7 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
 template <int LOG2N> constexpr int k2_tab_entries() { return (1 << LOG2N) / 2 + 1; }
 // k_cols runs at least two columns per workgroup, so that a Q row receives one
 // 16-B (or wider) piece per workgroup instead of one 8-B value per column
-template <int LOG2N> constexpr int k2_groups() { return groups_per_wg<LOG2N>() < 2 ? 2 : groups_per_wg<LOG2N>(); }
+template <int LOG2N> constexpr int k2_groups() { return groups_at_least<LOG2N, MM_K2_GROUPS>(); }
 template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * fft_T<LOG2N>(); }
 // dynamic LDS of k_cols: per group the FFT exchange buffer and its column's
 // per-bin table, plus one table for column N/2 (packed group only)
@@ -508,7 +567,7 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 // state buffer between frames.
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
-void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_t q_stride,
+void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
             const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
             Geo g, Spec sp, const c2 *__restrict__ tw)
 {
@@ -544,26 +603,91 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
     for (int j = 0; j < 8; ++j)
         prev[j] = state_in ? state_in[(size_t)f * N + t0 + j * T] : mk(0.0f, 0.0f);
 
-    for (int fr = 0; fr < nframes; ++fr) {
+    // G column of a frame: unconditional loads at clamped rows, selected at use.
+    // A frame's loads are issued before the previous frame's Q stores, so the
+    // wait for them does not wait for those stores (one in-order vmcnt).
+    c2 ga[8];
+    float gb[8];
+    // (buffer loads: 32-bit offsets, and kept in order with the buffer stores)
+    auto load_g = [&](int fr, int t) {
+        const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(G) + (size_t)gfr * g_stride, 0,
+                                                           (int)(g_stride * sizeof(c2)), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int rc = min(max(t + j * T - g.y0, 0), g.H - 1);
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, (unsigned)(f * g.H + rc) * 8u, 0, 0);
+            ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
+            gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, (unsigned)((N / 2) * g.H + rc) * 8u, 0, 0));
+        }
+    };
+    // twiddle bases of both FFTs, loaded once: no loads inside a frame but G's
+    c2 wtw[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    preload_twiddles<LOG2N, -1>(wtw, t0, tw);
+    constexpr int TK = q_tile<LOG2N>(), BLK = GPW * TK / 2;   // float4 per tile row
+    constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
+    const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
+    c2 *stg = lds_all;   // staged Q pieces of a frame: [Hq/TK][GPW][TK]
+    bool staged = false;   // stg holds the previous frame's pieces (uniform)
+
+    // One straight path per iteration: G loads of frame fr, then the Q stores
+    // of frame fr-1 from the staging buffer (exactly NST buffer stores per
+    // thread; slots past the end are dropped by the range check), then frame
+    // fr, whose first use of the loads waits with vmcnt(NST) and never for the
+    // stores.
+    for (int fr = 0;; ++fr) {
         // Opaque per-iteration copy of the lane index: stops LICM from hoisting
         // every t-derived LDS address and twiddle of both FFTs out of the frame
         // loop (that pinned ~200 VGPRs and capped occupancy at 1 wave/SIMD).
         int t = t0;
         asm volatile("" : "+v"(t));
-        const c2 *Gc = G + (size_t)fr * g_stride + (size_t)f * g.H;
-        const c2 *GN = G + (size_t)fr * g_stride + (size_t)(N / 2) * g.H;
+        load_g(fr < nframes ? fr : nframes - 1, t);
+        __builtin_amdgcn_sched_barrier(0);   // keep the stores behind the loads
+        {
+            float4 sv[NST];
+            unsigned so[NST];
+#pragma unroll
+            for (int i = 0; i < NST; ++i) {
+                const int e = grp * T + t + i * GPW * T;   // opaque t: not hoisted
+                const int kt = e / BLK, r = e - kt * BLK;
+                const bool ok = staged && e < nq &&
+                                (GPW <= N / 2 || fb + (2 * r) / TK < N / 2);   // tiny N: fewer columns than groups
+                sv[i] = reinterpret_cast<const float4 *>(stg)[ok ? e : 0];
+                so[i] = ok ? (unsigned)((kt * g.Qs + fb) * TK + 2 * r) * 8u : 0x80000000u;
+            }
+            __syncthreads();   // staging read before this frame's FFT rewrites the buffers
+            const int qfr = __builtin_amdgcn_readfirstlane(fr > 0 ? fr - 1 : 0);   // uniform
+            const auto qrs = __builtin_amdgcn_make_buffer_rsrc(
+                Q + (size_t)qfr * q_stride, 0, (int)(q_stride * sizeof(c2)), 0x00020000);
+#pragma unroll
+            for (int i = 0; i < NST; ++i) {
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 d = {__float_as_uint(sv[i].x), __float_as_uint(sv[i].y),
+                                 __float_as_uint(sv[i].z), __float_as_uint(sv[i].w)};
+                __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so[i], 0, 0);
+            }
+        }
+        if (fr == nframes) break;
+        // opaque per-iteration copy of the twiddle bases (same reason as t: the
+        // products of their powers must not be hoisted into live registers)
+        c2 wt[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            wt[i] = wtw[i];
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
+        }
         c2 v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {   // unconditional loads (clamped), then select
+        for (int j = 0; j < 8; ++j) {
             const int rr = t + j * T - g.y0;
-            const int rc = min(max(rr, 0), g.H - 1);
-            const c2 a = Gc[rc];
-            const float bn = GN[rc].x;
             const bool in = rr >= 0 && rr < g.H;
             // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
-            v[j] = in ? (packed ? mk(a.x, bn) : a) : mk(0.0f, 0.0f);
+            v[j] = in ? (packed ? mk(ga[j].x, gb[j]) : ga[j]) : mk(0.0f, 0.0f);
         }
-        fft_regs<LOG2N, -1>(v, t, lds, tw);
+        fft_regs_w<LOG2N, -1>(v, t, lds, wt);
         const bool pass_frame = fr == 0 && first_passthrough;
         if (blk0) {
             // packed group: Z = F0 + i FN.  Upper half of Z to LDS for the partner
@@ -609,13 +733,14 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
             }
             __syncthreads();   // the inverse FFT rewrites the buffer
         }
+        c2 *Qf = Q + (size_t)fr * q_stride;
+        staged = !pass_frame;
         if (pass_frame) {
             if (!packed) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) prev[j] = v[j];
             }
-            continue;
-        }
+        } else {
         if (!packed) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -627,7 +752,7 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        fft_regs<LOG2N, +1>(v, t, lds, tw);
+        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
         // Q is stored by row pairs (q_index) so that K3 reads each of its two
         // rows' values as one 16-B piece per bin, contiguous across the wave (a
         // column-major Q made K3's 16-B gathers cost it 4 of its 7 us/frame at
@@ -635,30 +760,21 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
         // (over the exchange buffers: every group has passed the barrier after
         // its last exchange read) and leave as one contiguous GPW*16-byte piece
         // per row pair; same-XCD workgroups complete the 128-B lines.
-        c2 *Qf = Q + (size_t)fr * q_stride;
-        c2 *stg = lds_all;   // [Hq/2][GPW][2]
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
             if (valid && k < g.Hq) {
-                const int s = ((k >> 1) * GPW) * 2 + (k & 1);
+                const int s = ((k / TK) * GPW) * TK + (k % TK);
                 if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
                     stg[s] = mk(v[j].x, 0.0f);
                     Qf[q_index(g, k, N / 2)] = mk(v[j].y, 0.0f);
                 } else {
-                    stg[s + 2 * grp] = v[j];
+                    stg[s + TK * grp] = v[j];
                 }
             }
         }
-        __syncthreads();
-        const int fb = blk * GPW;
-        for (int e = threadIdx.x; e < (g.Hq >> 1) * GPW; e += GPW * T) {
-            const int kp = e / GPW, c = e - kp * GPW;
-            if (GPW <= N / 2 || fb + c < N / 2)   // tiny N: fewer columns than groups
-                st_off<float4>(Qf, (unsigned)(kp * g.Qs + fb + c) * 16u,
-                               reinterpret_cast<const float4 *>(stg)[e]);
-        }
-        __syncthreads();   // the next frame's FFT rewrites the buffers
+        }   // !pass_frame
+        __syncthreads();   // staged pieces complete (stored at the top of the next iteration)
     }
     if (valid) {
         if (packed) {
@@ -691,29 +807,35 @@ void k_cols(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Q, size_
 // One FFT group per pair of Q list rows (ka, ka+1); list row k is canvas row
 // (rb + k) mod N.  PerformIFFT (.cs:563-620) ends in |z| (FFT.compute:143-150);
 // the horizontal half of ApplyAntiAliasing (.cs:428-429) follows.
+// One workgroup per Q tile (TK rows = GPW row pairs; pairs_per_frame = Hq/2
+// counts the tile padding, pairs at or past Hn/2 compute but store nothing).
 template <int LOG2N>
-__global__ __launch_bounds__(wg_threads<LOG2N>())
+__global__ __launch_bounds__(k3_threads<LOG2N>())
 void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Yh,
                 size_t yh_stride, int frame0, int pairs_per_frame, int total_pairs, Geo g,
                 Blur5 bw, const c2 *__restrict__ tw)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k3_groups<LOG2N>(), TK = q_tile<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    const int grp = GPW == 1 ? 0 : (T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T)
+                                               : threadIdx.x / T);
+    const int t = GPW == 1 ? threadIdx.x : threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
-    const bool valid = logical < total_pairs;
-    const int frame = frame0 + (valid ? logical / pairs_per_frame : 0);
-    const int ka = valid ? 2 * (logical % pairs_per_frame) : 0;
-    // row pair (ka, ka+1) of Q (q_index): one 16-B piece per bin, contiguous
-    const float4 *Qp = reinterpret_cast<const float4 *>(Q + (size_t)frame * q_stride) +
-                       (size_t)(ka >> 1) * g.Qs;
+    const int pair = logical % pairs_per_frame;
+    const bool valid = logical < total_pairs && 2 * pair < g.Hn;
+    const int frame = frame0 + (logical < total_pairs ? logical / pairs_per_frame : 0);
+    const int ka = 2 * pair;
+    // rows (ka, ka+1) of tile ka / TK: one 16-B piece per bin, TK*8 bytes apart
+    // across the wave; the workgroup's groups read the whole TK*8-byte blocks
+    const float4 *Qp = reinterpret_cast<const float4 *>(
+        Q + (size_t)frame * q_stride + (size_t)(ka / TK) * g.Qs * TK + (ka % TK));
     float4 qv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {   // all 8 loads in flight (addresses always valid)
         const int fq = t + j * T;
         const int ff = fq > N / 2 ? N - fq : fq;
-        qv[j] = Qp[ff];
+        qv[j] = Qp[(size_t)ff * (TK / 2)];
     }
     c2 v[8];
 #pragma unroll
