@@ -213,8 +213,14 @@ def main():
     stream = ShardedStream(backend, C, rank if ring else 0, world if ring else 1)
     torch.cuda.synchronize()
 
+    # ring mode overlaps each step's state shift with the previous step's
+    # compute (ShardedStream prefetch); the shift for a step past the end is
+    # never posted
+    def run_step(s):
+        stream.step(s, prefetch=ring and s + 1 < total_steps)
+
     for s in range(a.warmup):
-        stream.step(s)
+        run_step(s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -222,10 +228,11 @@ def main():
     h.profile_begin()
     t_start = time.perf_counter()
     for s in range(a.warmup, total_steps):
-        stream.step(s)
+        run_step(s)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     prof = h.profile_end()
+    stream.finish()
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

@@ -79,7 +79,7 @@ template <int LOG2N, int MIN> constexpr int groups_at_least() { return groups_at
 #define MM_K2_GROUPS 2
 #endif
 #ifndef MM_K3_GROUPS
-#define MM_K3_GROUPS 4
+#define MM_K3_GROUPS 1
 #endif
 // K3 runs one Q tile (TK = 2 * groups rows) per workgroup
 template <int LOG2N> constexpr int k3_groups() { return groups_at_least<LOG2N, MM_K3_GROUPS>(); }
@@ -134,6 +134,12 @@ __device__ __forceinline__ size_t q_index(const Geo &g, int k, int f)
 {
     return ((size_t)(k / g.TK) * g.Qs + f) * g.TK + (k % g.TK);
 }
+
+#ifdef MM_ASM_MARKS
+#define MM_MARK(x) asm volatile("; " x)
+#else
+#define MM_MARK(x)
+#endif
 
 // ---- pixel access -------------------------------------------------------
 template <int FMT> struct Pix;
@@ -687,7 +693,9 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
             v[j] = in ? (packed ? mk(ga[j].x, gb[j]) : ga[j]) : mk(0.0f, 0.0f);
         }
+        MM_MARK("M1_fwd_start");
         fft_regs_w<LOG2N, -1>(v, t, lds, wt);
+        MM_MARK("M2_fwd_end");
         const bool pass_frame = fr == 0 && first_passthrough;
         if (blk0) {
             // packed group: Z = F0 + i FN.  Upper half of Z to LDS for the partner
@@ -752,7 +760,9 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        MM_MARK("M3_inv_start");
         fft_regs_w<LOG2N, +1>(v, t, lds, wt);
+        MM_MARK("M4_inv_end");
         // Q is stored by row pairs (q_index) so that K3 reads each of its two
         // rows' values as one 16-B piece per bin, contiguous across the wave (a
         // column-major Q made K3's 16-B gathers cost it 4 of its 7 us/frame at

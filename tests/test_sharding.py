@@ -54,7 +54,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, chunk, steps, q):
+def _worker(rank, world, port, chunk, steps, q, prefetch=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -66,19 +66,23 @@ def _worker(rank, world, port, chunk, steps, q):
     ss = ShardedStream(OracleBackend(), chunk, rank, world)
     outs = {}
     for s in range(steps):
-        outs.update(ss.step(s))
+        outs.update(ss.step(s, prefetch=prefetch and s + 1 < steps))
+    ss.finish()
     q.put((rank, outs))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk,steps", [(2, 3, 3), (3, 2, 2)])
-def test_sharded_equals_single_stream(world, chunk, steps):
+@pytest.mark.parametrize("world,chunk,steps,prefetch", [(2, 3, 3, False), (3, 2, 2, False),
+                                                         (2, 2, 3, True), (3, 2, 3, True)])
+def test_sharded_equals_single_stream(world, chunk, steps, prefetch):
+    """prefetch: the ring shift of step s+1 is posted before step s's compute
+    (the overlapped form bench.py uses)."""
     from mm355.stream import ShardedStream
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, chunk, steps, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, chunk, steps, q, prefetch))
              for r in range(world)]
     for p in procs:
         p.start()
