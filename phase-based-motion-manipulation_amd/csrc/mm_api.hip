@@ -167,6 +167,8 @@ static void build_spec(const mm_params &p, int N, Spec &sp)
     sp.S = p.phase_scale;
     sp.tau2 = p.magnitude_threshold * p.magnitude_threshold;
     sp.inv_nn = 1.0f / ((float)N * (float)N);
+    sp.S_rev = (float)((double)p.phase_scale / (2.0 * 3.14159265358979323846));
+    sp.tau2_nn = sp.tau2 * sp.inv_nn * sp.inv_nn;   // exact: inv_nn is a power of two
     sp.hp_lo = p.max_freq * 0.8f;             // PyramidOperations.compute:36-41
     sp.hp_inv = 1.0f / (p.max_freq * 0.2f);
     sp.lp_hi = p.min_freq * 1.2f;             // PyramidOperations.compute:48-53

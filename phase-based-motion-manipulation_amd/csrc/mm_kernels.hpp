@@ -47,6 +47,8 @@ struct Spec {
     float bp_inv_low, bp_inv_1mhigh, bp_inv_band;
     int L;
     float minF, maxF, S, tau2, inv_nn;
+    float S_rev;            // S / (2 pi): phase scale in revolutions (v_sin/v_cos)
+    float tau2_nn;          // tau2 * inv_nn^2 (gate on masks pre-scaled by inv_nn)
     float hp_lo, hp_inv;    // high-pass ramp start maxF*0.8, 1/(maxF*0.2)
     float lp_hi, lp_inv;    // low-pass ramp end minF*1.2, 1/(minF*0.2)
     float lo[kMaxLevels], hi[kMaxLevels], inv_w[kMaxLevels];  // middle bands
@@ -490,7 +492,31 @@ __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
     }
 }
 
-// pyramid_op with the middle bands from the table (same arithmetic, same order)
+// atan2 for a nonzero argument (the magnified bins: |u| = |p||c| > 0 there)
+__device__ __forceinline__ float atan2_nz(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float a = fminf(ax, ay) * __builtin_amdgcn_rcpf(fmaxf(ax, ay));
+    const float s = a * a;
+    float r = -0.00405455008149147f;
+    r = r * s + 0.021862903609871864f;
+    r = r * s - 0.055912263691425323f;
+    r = r * s + 0.09642193466424942f;
+    r = r * s - 0.1390862911939621f;
+    r = r * s + 0.19946566224098206f;
+    r = r * s - 0.33329859375953674f;
+    r = r * s + 0.9999993443489075f;
+    r *= a;
+    if (ay > ax) r = 1.57079632679489662f - r;
+    if (x < 0.0f) r = 3.14159265358979324f - r;
+    return copysignf(r, y);
+}
+
+// pyramid_op with the middle bands from the table.  Table entries are the
+// masks times inv_nn = 1/N^2 (a power of two, so every product and sum below
+// is the unscaled one times inv_nn exactly, and the gate m^2 mn2 < tau^2 reads
+// (m inv_nn)^2 mn2 < tau^2 inv_nn^2 with the same outcome):
+//   A = c * [mpass + mmag e^{i S delta}],  delta = arg(p conj c)
 template <int LOG2N>
 __device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spec &sp, float2 mt)
 {
@@ -507,21 +533,21 @@ __device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spe
         mpass = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
         if (sp.L > 1)
             mpass += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+        mpass *= sp.inv_nn;
         mb = mt.y;
     }
     float mmag = 0.0f;
-    if (mt.x * mt.x * mn2 < sp.tau2) mpass += mt.x;
+    if (mt.x * mt.x * mn2 < sp.tau2_nn) mpass += mt.x;
     else mmag += mt.x;
-    if (mb * mb * mn2 < sp.tau2) mpass += mb;
+    if (mb * mb * mn2 < sp.tau2_nn) mpass += mb;
     else mmag += mb;
-    c2 a = scale(c, mpass * sp.inv_nn);
+    c2 w = mk(mpass, 0.0f);
     if (mmag > 0.0f) {
-        const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
-        const float ph = sp.S * d;
-        const float k = mmag * sp.inv_nn;
-        a = add(a, scale(mul(c, mk(__cosf(ph), __sinf(ph))), k));
+        // S * delta in revolutions straight into v_sin / v_cos
+        const float rev = atan2_nz(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y) * sp.S_rev;
+        w = mk(mmag * __builtin_amdgcn_cosf(rev) + mpass, mmag * __builtin_amdgcn_sinf(rev));
     }
-    return a;
+    return mul(c, w);
 }
 
 template <int MODE>
@@ -598,8 +624,14 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
 
     if constexpr (MODE != MM_MODE_PYRAMID) {
         for (int e = t0; e < TE; e += T) {
-            tab0[e] = bin_static<LOG2N, MODE>(f, e, sp);
-            if (packed) tabN[e] = bin_static<LOG2N, MODE>(N / 2, e, sp);
+            // pyramid table: masks pre-scaled by inv_nn (a power of two: exact)
+            const float ks = MODE == MM_K2_PYR_TAB ? sp.inv_nn : 1.0f;
+            const float2 b0 = bin_static<LOG2N, MODE>(f, e, sp);
+            tab0[e] = make_float2(b0.x * ks, b0.y * ks);
+            if (packed) {
+                const float2 bn = bin_static<LOG2N, MODE>(N / 2, e, sp);
+                tabN[e] = make_float2(bn.x * ks, bn.y * ks);
+            }
         }
         __syncthreads();
     }
@@ -613,7 +645,7 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
     // A frame's loads are issued before the previous frame's Q stores, so the
     // wait for them does not wait for those stores (one in-order vmcnt).
     c2 ga[8];
-    float gb[8];
+    float gb[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     // (buffer loads: 32-bit offsets, and kept in order with the buffer stores)
     auto load_g = [&](int fr, int t) {
         const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform
@@ -625,7 +657,14 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, (unsigned)(f * g.H + rc) * 8u, 0, 0);
             ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
-            gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, (unsigned)((N / 2) * g.H + rc) * 8u, 0, 0));
+        }
+        if (blk0) {   // column N/2 (real) for the packed group's block only
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int rc = min(max(t + j * T - g.y0, 0), g.H - 1);
+                gb[j] = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(grs, (unsigned)((N / 2) * g.H + rc) * 8u, 0, 0));
+            }
         }
     };
     // twiddle bases of both FFTs, loaded once: no loads inside a frame but G's
