@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--mode", choices=("ring", "replicas"), default="ring")
     ap.add_argument("--standard", action="store_true",
                     help="usePyramidDecomposition=false (standard mode, SURVEY f1)")
+    ap.add_argument("--orientations", type=int, default=1,
+                    help=">1: MM_MODE_STEERABLE extension (SURVEY f2; BASELINE's "
+                         "'8-orientation' wording), 4/6/8 oriented subbands per level")
+    ap.add_argument("--temporal-filter", choices=("diff", "iir"), default="diff",
+                    help="steerable extension's temporal filter (iir: no ring mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="bound on the CPU-baseline sample")
@@ -194,8 +199,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     W, H, C = a.width, a.height, a.frames_per_step
     os.environ.setdefault("MM_CHUNK", str(C))
-    params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
-                               mode=mm355.MODE_STANDARD if a.standard else mm355.MODE_PYRAMID)
+    steer = a.orientations > 1
+    if steer:
+        params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
+                                   mode=mm355.MODE_STEERABLE, orientations=a.orientations,
+                                   temporal_filter=1 if a.temporal_filter == "iir" else 0)
+    else:
+        params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
+                                   mode=mm355.MODE_STANDARD if a.standard else mm355.MODE_PYRAMID)
     h = mm355.Handle(W, H, params, device=local)
     N = h.N
 
@@ -244,12 +255,13 @@ def main():
     kern = {}
     for name, (ms, launches, nfr) in prof.items():
         if launches:
-            ab = compulsory_bytes(W, H, N, nfr // launches)[name]
+            ab = compulsory_bytes(W, H, N, nfr // launches).get(name) if not steer else None
             kern[name] = {"ms_total": round(ms, 4), "launches": launches, "frames": nfr,
                           "us_per_frame": round(ms * 1e3 / nfr, 3),
                           "ms_per_launch": round(ms / launches, 5),
                           "algorithmic_bytes_per_launch": ab,
-                          "achieved_GBps": round(ab / (ms / launches * 1e-3) / 1e9, 1)}
+                          "achieved_GBps": (round(ab / (ms / launches * 1e-3) / 1e9, 1)
+                                            if ab else None)}
     dom = max(kern, key=lambda k: kern[k]["ms_total"])
     dk = kern[dom]
     achieved = dk["achieved_GBps"]
@@ -279,7 +291,10 @@ def main():
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": (f"{W}x{H} RGBA8 synthetic stream, standard (non-pyramid) mode, "
+        "config": {"workload": (f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level steerable "
+                                f"extension, {a.orientations} orientations, {a.temporal_filter} "
+                                f"temporal filter, PhaseScale={a.phase_scale}" if steer else
+                                f"{W}x{H} RGBA8 synthetic stream, standard (non-pyramid) mode, "
                                 f"PhaseScale={a.phase_scale}" if a.standard else
                                 f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
                                 f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)"),
@@ -288,7 +303,8 @@ def main():
                                    if ring else f"replicas x{world}")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 5) if achieved else None,
+                     "traffic": traffic,
                      "bytes_model": "compulsory bytes of the dominant kernel (DESIGN.md §5); "
                                     "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch",
                      "compute": valu},
@@ -300,7 +316,7 @@ def main():
         "kernels": kern,
     }
     h.close()
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not steer:
         result["cpu_baseline"], ref = cpu_baseline(W, H, a.levels, a.phase_scale,
                                                    a.cpu_seconds, a.standard)
         result["parity_vs_oracle"] = parity_check(mm355, torch, params, W, H, ref, local)

@@ -11,4 +11,6 @@ timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/$
 cat gpurun_out/${TAG}_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err || { echo PROF FAIL; exit 1; }
 bash scripts/gpu_pmc.sh ${TAG}_pmc || { echo PMC FAIL; exit 1; }
+bash scripts/gpu_stall.sh ${TAG}_st > /dev/null || { echo STALL FAIL; exit 1; }
+python3 tools/valu_summary.py gpurun_out/${TAG}_st_1,gpurun_out/${TAG}_st_2 gpurun_out/${TAG}_prof gpurun_out/${TAG}_valu.json
 echo ALL OK

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU issue utilisation per kernel from rocprofv3 PMC + kernel-trace runs.
 
-usage: valu_summary.py PMC_DIR KERNEL_TRACE_DIR OUT_JSON
+usage: valu_summary.py PMC_DIR[,PMC_DIR...] KERNEL_TRACE_DIR OUT_JSON
 
 valu_busy = SQ_INSTS_VALU * 4 cycles / (SIMDs * kernel cycles), with the
 kernel's cycles from its average kernel-trace duration and the shader clock
@@ -26,7 +26,7 @@ def short(name):
 
 
 pmc = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+for f in [f for d in sys.argv[1].split(",") for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True)]:
     for r in csv.DictReader(open(f)):
         k = short(r["Kernel_Name"])
         if k:
