@@ -49,7 +49,7 @@ struct mm_handle {
     float *d_dbg;               // debug view textures [chunk][mag, phase][N][N] (lazily)
     // MM_MODE_STEERABLE (lazily, for the current levels/orientations):
     c2 *d_Fb;                   // per chunk frame half spectrum [chunk][N/2+1][N]
-    c2 *d_T;                    // band columns [nb+1][N][Hq]
+    c2 *d_T;                    // band rows [nb+1][Hq][N] (row-major, k_sb_cols -> k_sb_rows)
     float *d_sst;               // temporal-filter state: phi, u_h, u_l planes [nb][Hn][W+4]
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
     bool steer_valid;           // d_sst holds the state after the previous frame
@@ -431,9 +431,10 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         const int reset = k < seed;
         {
             ProfScope ps(h, s, MM_K_COLS, 0);
-            hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + gpw - 1) / gpw), dim3(wg_threads<LOG2N>()),
-                               lds, s, h->d_Fb + fstride * k, h->d_T, band_stride, h->geo, h->spec,
-                               h->d_tw);
+            const int g2 = k2_groups<LOG2N>();
+            hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(k2_threads<LOG2N>()),
+                               sizeof(c2) * (size_t)g2 * lds_complex<N>(), s, h->d_Fb + fstride * k,
+                               h->d_T, band_stride, h->geo, h->spec, h->d_tw);
             HIPCHK(hipGetLastError());
         }
         ProfScope ps(h, s, MM_K_ROWS_INV, reset || !write ? 0 : 1);

@@ -7,8 +7,8 @@
 //   k_cols_fwd : G columns -> F, the half spectrum (f <= N/2, all fy)
 //   k_sb_cols  : one column kx of F (Hermitian mirror for kx > N/2) times each
 //                band mask  m_i a_o / N^2  (o < O/2) and the residual mask
-//                (m_0 + m_{L-1}) / N^2 -> column IFFT -> T[band][kx][k] for
-//                the Hn list rows the crop + blur need
+//                (m_0 + m_{L-1}) / N^2 -> column IFFT -> T[band][k][kx] (row-major)
+//                for the Hn list rows the crop + blur need
 //   k_sb_rows  : one list row k: per band the row IFFT -> local coefficient
 //                s(x); in the W+4 columns the blur reads, phase filter vs the
 //                state, s' = s e^{i S P} (gated |s| < tau), y += 2 Re s';
@@ -80,18 +80,26 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
 }
 
 // -------------------------------------------------------------------------
-// Band columns: T[b][kx][k] = IFFT_col(F m_i a_o / N^2)[canvas row rb + k]
+// Band columns: T[b][k][kx] = IFFT_col(F m_i a_o / N^2)[canvas row rb + k]
 // -------------------------------------------------------------------------
+// GPW >= 2 columns per workgroup (same-XCD blocks own consecutive columns):
+// each band's columns are transposed through LDS and leave as one GPW*8-byte
+// piece per row of the row-major T, which k_sb_rows then reads contiguously
+// (a column-major T made those reads 8-B gathers: 16x L2->L1 traffic).  The
+// band loop issues no loads (twiddle bases hoisted), so its stores are never
+// waited for.
 template <int LOG2N>
-__global__ __launch_bounds__(wg_threads<LOG2N>())
+__global__ __launch_bounds__(k2_threads<LOG2N>())
 void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_stride, Geo g, Spec sp,
                const c2 *__restrict__ tw)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
+    const int t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
-    const int kx_raw = blockIdx.x * GPW + grp;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int kx_raw = blk * GPW + grp;
     const bool valid = kx_raw < N;               // small N: more groups than columns
     const int kx = valid ? kx_raw : N - 1;
     const bool mir = kx > N / 2;
@@ -116,12 +124,25 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
         for (int k = 0; k < sp.O; ++k) sum += pow4(fmaxf(0.0f, cx[j] * sp.ang_c[k] + sy[j] * sp.ang_s[k]));
         isum[j] = flat ? -1.0f : 1.0f / sum;
     }
+    c2 wtw[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    preload_twiddles<LOG2N, -1>(wtw, t0, tw);
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
+    const int kx0 = blk * GPW;
+    c2 *stg = lds_all;   // [Hn][GPW]
     for (int b = 0; b <= nb; ++b) {
-        // opaque lane index per band: keeps LICM from hoisting the FFT addressing
+        // opaque lane index and twiddle bases per band: keeps LICM from
+        // hoisting the FFT addressing and twiddle powers into live registers
         int t = t0;
         asm volatile("" : "+v"(t));
+        c2 wt[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            wt[i] = wtw[i];
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
+        }
         const int o = nmid ? b / nmid : 0, i = nmid ? 1 + b % nmid : 0;
         c2 v[8];
 #pragma unroll
@@ -137,13 +158,29 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
             }
             v[j] = scale(v0[j], m);
         }
-        fft_regs<LOG2N, +1>(v, t, lds, tw);
-        c2 *out = Tb + (size_t)b * band_stride + (size_t)kx * g.Hq;
+        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
+        // every group has passed the barrier after its last exchange read
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-            if (valid && k < g.Hn) out[k] = v[j];
+            if (k < g.Hn) stg[k * GPW + grp] = v[j];
         }
+        __syncthreads();
+        c2 *out = Tb + (size_t)b * band_stride;
+        if constexpr (GPW <= N) {   // whole pieces: GPW / 2 float4 per row
+            constexpr int PW = GPW / 2;
+            for (int e = grp * T + t; e < g.Hn * PW; e += GPW * T) {
+                const int k = e / PW, part = e - k * PW;
+                *reinterpret_cast<float4 *>(out + (size_t)k * N + kx0 + 2 * part) =
+                    reinterpret_cast<const float4 *>(stg)[e];
+            }
+        } else {                    // tiny N: fewer columns than groups
+            for (int e = grp * T + t; e < g.Hn * GPW; e += GPW * T) {
+                const int k = e / GPW, c = e - k * GPW;
+                if (kx0 + c < N) out[(size_t)k * N + kx0 + c] = stg[e];
+            }
+        }
+        __syncthreads();   // the next band's FFT rewrites the buffers
     }
 }
 
@@ -153,10 +190,15 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 // State planes (floats): phi[b][k][xi], u_h[...], u_l[...] for the Wc = W+4
 // canvas columns x0-2 .. x0+W+1 the horizontal blur reads (xi = x - (x0-2)
 // mod N).  reset: first frame (phi <- arg s, u <- 0, nothing amplified).
+// Band b+1's row loads are issued before band b's state stores, so the FFT's
+// wait for them does not wait for those stores (one in-order vmcnt); band
+// b+1's state loads follow the stores and are consumed only after its FFT,
+// when the stores have long completed.  The pointers are not restrict so
+// that the compiler keeps this order.
 template <int LOG2N>
 __global__ __launch_bounds__(wg_threads<LOG2N>())
-void k_sb_rows(const c2 *__restrict__ Tb, size_t band_stride, float *__restrict__ Yh,
-               float *__restrict__ st_phi, float *__restrict__ st_uh, float *__restrict__ st_ul,
+void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
+               float *st_phi, float *st_uh, float *st_ul,
                int reset, int write_out, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
@@ -169,54 +211,102 @@ void k_sb_rows(const c2 *__restrict__ Tb, size_t band_stride, float *__restrict_
     const int Wc = g.W + 4, xs = g.x0 - 2;
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
+    const bool iir = sp.filt == MM_FILTER_IIR;
+    c2 wtw[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    preload_twiddles<LOG2N, -1>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
+    // row k of band b (contiguous) and its state: loaded one band ahead
+    c2 v[8];
+    float pp[8], puh[8], pul[8];
+    auto load_row = [&](int b, int t) {
+        const c2 *row = Tb + (size_t)b * band_stride + (size_t)k * N;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = row[t + j * T];
+    };
+    auto load_state = [&](int b, int t) {
+        if (b < nb && !reset) {
+            const size_t rs = ((size_t)b * g.Hn + k) * Wc;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int xi = min((t + j * T - xs + N) & (N - 1), Wc - 1);
+                pp[j] = st_phi[rs + xi];
+                if (iir) {
+                    puh[j] = st_uh[rs + xi];
+                    pul[j] = st_ul[rs + xi];
+                }
+            }
+        }
+    };
+    {
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        load_row(0, t);
+        load_state(0, t);
+    }
     float y[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) y[j] = 0.0f;
     for (int b = 0; b <= nb; ++b) {
         int t = t0;
         asm volatile("" : "+v"(t));
-        const c2 *col = Tb + (size_t)b * band_stride + k;
-        c2 v[8];
+        c2 wt[16];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = col[(size_t)(t + j * T) * g.Hq];
-        fft_regs<LOG2N, +1>(v, t, lds, tw);
+        for (int i = 0; i < 16; ++i) {
+            wt[i] = wtw[i];
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
+        }
+        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
         if (b == nb) {   // residual: Hermitian, real output
 #pragma unroll
             for (int j = 0; j < 8; ++j) y[j] += v[j].x;
-            continue;
+            break;
         }
-        const size_t row = ((size_t)b * g.Hn + k) * Wc;
+        // this band's new state and amplified synthesis, in registers
+        float nph[8], nuh[8], nul[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+            const float ph = fast_atan2(v[j].y, v[j].x);
+            float P = 0.0f, uh = 0.0f, ul = 0.0f;
+            if (!reset) {
+                if (!iir) {
+                    P = wrap_pi(pp[j] - ph);              // prev - cur, as the reference
+                } else {
+                    const float d = wrap_pi(ph - pp[j]);
+                    uh = (1.0f - sp.r_high) * (puh[j] + d);
+                    ul = (1.0f - sp.r_low) * (pul[j] + d);
+                    P = ul - uh;
+                }
+            }
+            nph[j] = ph;
+            nuh[j] = uh;
+            nul[j] = ul;
+            c2 s2 = v[j];
+            if (write_out && v[j].x * v[j].x + v[j].y * v[j].y >= sp.tau2) {
+                const float rev = P * sp.S_rev;
+                s2 = mul(v[j], mk(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)));
+            }
             const int xi = (t + j * T - xs + N) & (N - 1);
-            if (valid && xi < Wc) {
-                const size_t si = row + xi;
-                const float ph = atan2f(v[j].y, v[j].x);
-                float P = 0.0f, uh = 0.0f, ul = 0.0f;
-                if (!reset) {
-                    const float pp = st_phi[si];
-                    if (sp.filt == MM_FILTER_DIFF) {
-                        P = wrap_pi(pp - ph);              // prev - cur, as the reference
-                    } else {
-                        const float d = wrap_pi(ph - pp);
-                        uh = (1.0f - sp.r_high) * (st_uh[si] + d);
-                        ul = (1.0f - sp.r_low) * (st_ul[si] + d);
-                        P = ul - uh;
+            if (xi < Wc) y[j] += 2.0f * s2.x;
+        }
+        load_row(b + 1, t);
+        __builtin_amdgcn_sched_barrier(0);   // row loads of b+1 ahead of the stores of b
+        if (valid) {
+            const size_t rs = ((size_t)b * g.Hn + k) * Wc;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int xi = (t + j * T - xs + N) & (N - 1);
+                if (xi < Wc) {
+                    st_phi[rs + xi] = nph[j];
+                    if (iir) {
+                        st_uh[rs + xi] = nuh[j];
+                        st_ul[rs + xi] = nul[j];
                     }
                 }
-                st_phi[si] = ph;
-                if (sp.filt == MM_FILTER_IIR) {
-                    st_uh[si] = uh;
-                    st_ul[si] = ul;
-                }
-                c2 s2 = v[j];
-                if (write_out && v[j].x * v[j].x + v[j].y * v[j].y >= sp.tau2) {
-                    const float a = sp.S * P;
-                    s2 = mul(v[j], mk(__cosf(a), __sinf(a)));
-                }
-                y[j] += 2.0f * s2.x;
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
+        load_state(b + 1, t);
     }
     if (!write_out) return;
     // |y| (ConvertComplexMagToTex) then the horizontal half of ApplyAntiAliasing
