@@ -68,6 +68,13 @@ def parse():
                          "'8-orientation' wording), 4/6/8 oriented subbands per level")
     ap.add_argument("--temporal-filter", choices=("diff", "iir"), default="diff",
                     help="steerable extension's temporal filter (iir: no ring mode)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="gloo: rehearsal of the N>1 path without RCCL (ranks may share one "
+                         "GPU; the ring state goes through host memory)")
+    ap.add_argument("--checksum", action="store_true",
+                    help="rehearsal: print per-frame output checksums (all ranks, rank 0) "
+                         "instead of the bench line; sharded and single-rank runs of the "
+                         "same frames must agree bitwise")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="bound on the CPU-baseline sample")
@@ -77,9 +84,11 @@ def parse():
 class GpuBackend:
     """ShardedStream backend over one mm355 handle; frames pre-generated."""
 
-    def __init__(self, handle, frames, out, fmt, chunk, world, rank, torch):
+    def __init__(self, handle, frames, out, fmt, chunk, world, rank, torch, host_exchange=False):
         self.h, self.frames, self.out, self.fmt = handle, frames, out, fmt
         self.chunk, self.world, self.rank, self.torch = chunk, world, rank, torch
+        self.host = host_exchange     # gloo rehearsal: exchanged states live on the host
+        self.sums = None              # --checksum: global frame index -> byte sum
 
     def _stream(self):
         return self.torch.cuda.current_stream().cuda_stream
@@ -89,16 +98,19 @@ class GpuBackend:
         return step, frame_index - step * self.world * self.chunk - self.rank * self.chunk
 
     def empty_state(self):
-        return self.torch.empty(self.h.state_bytes, dtype=self.torch.uint8, device="cuda")
+        return self.torch.empty(self.h.state_bytes, dtype=self.torch.uint8,
+                                device="cpu" if self.host else "cuda")
 
     def state_of(self, frame_index):
         s, k = self._local(frame_index)
-        buf = self.empty_state()
+        buf = self.torch.empty(self.h.state_bytes, dtype=self.torch.uint8, device="cuda")
         self.h.compute_state(self.frames[s % len(self.frames), k], self.fmt, buf,
                              stream=self._stream())
-        return buf
+        return buf.cpu() if self.host else buf
 
     def set_state(self, buf):
+        if self.host:
+            buf = buf.cuda()
         self.h.set_state(buf, stream=self._stream())
 
     def reset(self):
@@ -108,6 +120,10 @@ class GpuBackend:
         s, k = self._local(lo)
         self.h.process_stream(self.frames[s % len(self.frames), k], self.out, count, self.fmt,
                               stream=self._stream())
+        if self.sums is not None:
+            v = self.out[:count].reshape(count, -1).sum(dim=1, dtype=self.torch.int64).cpu()
+            for i in range(count):
+                self.sums[lo + i] = int(v[i])
 
 
 def _cpu_model():
@@ -194,9 +210,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    gloo = a.dist_backend == "gloo"
+    # gloo rehearsal: ranks may share the box's GPU(s)
+    dev = local % torch.cuda.device_count() if gloo else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     W, H, C = a.width, a.height, a.frames_per_step
     os.environ.setdefault("MM_CHUNK", str(C))
     steer = a.orientations > 1
@@ -207,7 +229,7 @@ def main():
     else:
         params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
                                    mode=mm355.MODE_STANDARD if a.standard else mm355.MODE_PYRAMID)
-    h = mm355.Handle(W, H, params, device=local)
+    h = mm355.Handle(W, H, params, device=dev)
     N = h.N
 
     # resident inputs: one buffer per step (warmup + timed), generated on device
@@ -220,8 +242,10 @@ def main():
         h.synth(frames[s], t0, C, seed=seed, stream=torch.cuda.current_stream().cuda_stream)
     out = torch.empty((C, H, W, 4), dtype=torch.uint8, device="cuda")
     backend = GpuBackend(h, frames, out, mm355.RGBA8, C, world if ring else 1,
-                         rank if ring else 0, torch)
+                         rank if ring else 0, torch, host_exchange=gloo)
     stream = ShardedStream(backend, C, rank if ring else 0, world if ring else 1)
+    if a.checksum:
+        backend.sums = {}
     torch.cuda.synchronize()
 
     # ring mode overlaps each step's state shift with the previous step's
@@ -244,9 +268,22 @@ def main():
     elapsed = time.perf_counter() - t_start
     prof = h.profile_end()
     stream.finish()
+    if a.checksum:
+        sums = backend.sums
+        if world > 1:
+            allv = [None] * world
+            dist.all_gather_object(allv, sums)
+            sums = {k: v for d in allv for k, v in d.items()}
+        if rank == 0:
+            print(json.dumps({"checksums": [sums[k] for k in sorted(sums)],
+                              "frames": sorted(sums)[:1] + sorted(sums)[-1:], "world": world}),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -299,7 +336,9 @@ def main():
                                 f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
                                 f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)"),
                    "frames_per_step_per_gpu": C, "padded_n": N,
-                   "parallelism": (f"frame-sharded x{world}, RCCL ring state shift"
+                   "parallelism": (f"frame-sharded x{world}, "
+                                   + ("gloo rehearsal, ring state via host" if gloo
+                                      else "RCCL ring state shift")
                                    if ring else f"replicas x{world}")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -4,6 +4,7 @@ Bars: fp32 max-abs <= 1e-4 and RMSE <= 1e-5 at integer phase
 scale; 99.9th percentile <= 1e-4 at non-integer scale; RGBA8 exact except
 +-1 LSB on <= 0.1% of values; first frame bitwise.
 """
+import os
 import numpy as np
 import pytest
 
@@ -365,3 +366,29 @@ def test_1080p_stream_device_synth_u8():
     assert np.array_equal(got[0], ref[0])
     for k in range(1, n):
         T.assert_close_u8(got[k], ref[k])
+
+
+@pytest.mark.gpu
+def test_bench_sharded_ring_equals_single_rank():
+    """bench.py's own N>1 path (ShardedStream with prefetch, GpuBackend state
+    hand-off via mm_compute_state/mm_set_state) at world 2 over gloo on this
+    GPU (the ring state through host memory instead of RCCL): per-frame output
+    checksums equal the single-rank run of the same 48 frames bitwise."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(cmd):
+        out = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+        assert out.returncode == 0, out.stderr[-2000:]
+        return json.loads([l for l in out.stdout.splitlines() if l.startswith('{"')][-1])
+
+    one = run([sys.executable, "bench.py", "--checksum", "--frames-per-step", "12",
+               "--steps", "3", "--warmup", "1"])
+    two = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", "29541", "bench.py", "--gpus", "2",
+               "--dist-backend", "gloo", "--checksum", "--frames-per-step", "6", "--steps", "3",
+               "--warmup", "1"])
+    assert one["frames"] == two["frames"] == [0, 47]
+    assert one["checksums"] == two["checksums"]
