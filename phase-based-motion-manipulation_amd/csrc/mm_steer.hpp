@@ -47,6 +47,18 @@ template <int N> __device__ __forceinline__ float sfreq(int k)
     return (float)(k < N / 2 ? k : k - N) * (1.0f / (float)N);
 }
 
+// Band b (< nb) of column kx is identically zero when the column lies outside
+// the band's annulus: every bin has fr >= |fx| (exact in fp32: fx = k/N and
+// sqrt of the exact square), and level_mask is 0 for fr > hi.  Both band
+// kernels apply this same test: k_sb_cols skips such columns (no FFT, no
+// store) and k_sb_rows reads zeros for them (no load).  For L = 5 the two
+// inner levels' bands are zero in 55 % and 85 % of the columns.
+template <int N>
+__device__ __forceinline__ bool band_col_zero(int b, int nb, int nmid, int kx, const Spec &sp)
+{
+    return b < nb && fabsf(sfreq<N>(kx)) > sp.hi[1 + b % nmid];
+}
+
 // -------------------------------------------------------------------------
 // F of every chunk frame: column FFTs of K1's G, stored as Fb[fr][f][fy].
 // -------------------------------------------------------------------------
@@ -144,6 +156,10 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
             if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
         }
         const int o = nmid ? b / nmid : 0, i = nmid ? 1 + b % nmid : 0;
+        // workgroup-uniform: skip the band where all its columns are zero
+        bool all_zero = true;
+        for (int c = 0; c < GPW && kx0 + c < N; ++c) all_zero &= band_col_zero<N>(b, nb, nmid, kx0 + c, sp);
+        if (all_zero) continue;
         c2 v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -222,7 +238,8 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     auto load_row = [&](int b, int t) {
         const c2 *row = Tb + (size_t)b * band_stride + (size_t)k * N;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = row[t + j * T];
+        for (int j = 0; j < 8; ++j)   // band_col_zero columns were never written: 0
+            v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp) ? mk(0.0f, 0.0f) : row[t + j * T];
     };
     auto load_state = [&](int b, int t) {
         if (b < nb && !reset) {
