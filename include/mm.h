@@ -69,8 +69,8 @@ typedef struct {
     float max_freq;            /* maxFrequency             .cs:21               */
     float phase_scale;         /* phaseScale (PhaseScale)  .cs:29               */
     float magnitude_threshold; /* magnitudeThreshold=0.01  .cs:30               */
-    int   orientations;        /* extension; must be 1 (reference semantics)    */
-    int   mode;                /* MM_MODE_PYRAMID | MM_MODE_STANDARD            */
+    int   orientations;        /* 1 (reference semantics); 4, 6, 8 with MM_MODE_STEERABLE */
+    int   mode;                /* MM_MODE_PYRAMID | MM_MODE_STANDARD | MM_MODE_STEERABLE */
     int   edge_mode;           /* MM_EDGE_REPEAT | MM_EDGE_CLAMP                */
     int   apply_magnification; /* applyMotionMagnification .cs:12 (0: passthrough) */
     /* standard mode's phase-delta band-pass (PhaseDifferenceComputeShader.compute:88-122) */

@@ -580,12 +580,15 @@ template <int LOG2N> constexpr int k2_tab_entries() { return (1 << LOG2N) / 2 + 
 template <int LOG2N> constexpr int k2_groups() { return groups_at_least<LOG2N, MM_K2_GROUPS>(); }
 template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * fft_T<LOG2N>(); }
 // dynamic LDS of k_cols: per group the FFT exchange buffer and its column's
-// per-bin table, plus one table for column N/2 (packed group only)
+// per-bin table, plus for column N/2 (packed group only) its table, its
+// previous spectrum (bins 0..N/2) and its staged Q values (one float per row).
+// Above 64 KiB at N = 2048 (77.8 KiB): two workgroups still fit a CU's 160 KiB.
 template <int LOG2N> constexpr size_t k2_lds_bytes()
 {
     return (size_t)k2_groups<LOG2N>() *
                (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_entries<LOG2N>()) +
-           sizeof(float2) * k2_tab_entries<LOG2N>();
+           sizeof(float2) * k2_tab_entries<LOG2N>() + sizeof(c2) * ((1 << LOG2N) / 2 + 1) +
+           sizeof(float) * (1 << LOG2N);
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
@@ -612,6 +615,11 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
     c2 *lds = lds_all + grp * lds_complex<N>();
     float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TE;
     float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TE;
+    // column N/2: F_{t-1} at bins 0..N/2 between frames, and one frame's Q
+    // values by list row (staged like the others: no global round trip and no
+    // store the next frame's loads must wait for)
+    c2 *ldsN = reinterpret_cast<c2 *>(tabN + TE);
+    float *stgN = reinterpret_cast<float *>(ldsN + N / 2 + 1);
     // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
     // are merged in one L2 (split over XCDs they left as partial-line writes)
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -640,6 +648,14 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
 #pragma unroll
     for (int j = 0; j < 8; ++j)
         prev[j] = state_in ? state_in[(size_t)f * N + t0 + j * T] : mk(0.0f, 0.0f);
+    if (packed) {   // each thread reads and writes only its own bins: no barrier
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int fy = t0 + j * T;
+            if (j < 4 || fy == N / 2)
+                ldsN[fy] = state_in ? state_in[(size_t)(N / 2) * N + fy] : mk(0.0f, 0.0f);
+        }
+    }
 
     // G column of a frame: unconditional loads at clamped rows, selected at use.
     // A frame's loads are issued before the previous frame's Q stores, so the
@@ -714,6 +730,20 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                                  __float_as_uint(sv[i].z), __float_as_uint(sv[i].w)};
                 __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so[i], 0, 0);
             }
+            // column N/2 of frame fr-1 (block 0 only; elsewhere dropped stores
+            // keep the count static).  Read after the barrier: stgN is rewritten
+            // only after the packed section's first barrier below.
+            constexpr int NSTN = (N / 2 + GPW * T - 1) / (GPW * T);
+#pragma unroll
+            for (int i = 0; i < NSTN; ++i) {
+                const int e = grp * T + t + i * GPW * T;
+                const bool ok = staged && blk0 && e < g.Hq / 2;   // rows 2e, 2e+1 (one tile: TK even)
+                const float2 p = reinterpret_cast<const float2 *>(stgN)[ok ? e : 0];
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 d = {__float_as_uint(p.x), 0u, __float_as_uint(p.y), 0u};
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    d, qrs, ok ? (unsigned)(((2 * e) / TK * g.Qs + N / 2) * TK + (2 * e) % TK) * 8u : 0x80000000u, 0, 0);
+            }
         }
         if (fr == nframes) break;
         // opaque per-iteration copy of the twiddle bases (same reason as t: the
@@ -745,7 +775,6 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             }
             __syncthreads();
             if (packed) {
-                const c2 *pNsrc = fr ? stN : (state_in ? state_in + (size_t)(N / 2) * N : nullptr);
 #pragma unroll
                 for (int j = 0; j < 5; ++j) {
                     __builtin_amdgcn_sched_barrier(0);
@@ -757,7 +786,7 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                         const c2 f0 = mk(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
                         const c2 fN = mk(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
                         if (!pass_frame) {
-                            const c2 pn = pNsrc ? pNsrc[fy] : mk(0.0f, 0.0f);
+                            const c2 pn = ldsN[fy];
                             const c2 a0 = k2_op<LOG2N, MODE>(f0, prev[j], 0, fy, sp, tab0);
                             const c2 an = k2_op<LOG2N, MODE>(fN, pn, N / 2, fy, sp, tabN);
                             v[j] = mk(a0.x - an.y, a0.y + an.x);   // A0 + i AN
@@ -765,7 +794,7 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                                 lds[pad8(fy)] = mk(a0.x + an.y, an.x - a0.y);
                         }
                         prev[j] = f0;
-                        stN[fy] = fN;
+                        ldsN[fy] = fN;
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -780,7 +809,6 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             }
             __syncthreads();   // the inverse FFT rewrites the buffer
         }
-        c2 *Qf = Q + (size_t)fr * q_stride;
         staged = !pass_frame;
         if (pass_frame) {
             if (!packed) {
@@ -816,7 +844,7 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                 const int s = ((k / TK) * GPW) * TK + (k % TK);
                 if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
                     stg[s] = mk(v[j].x, 0.0f);
-                    Qf[q_index(g, k, N / 2)] = mk(v[j].y, 0.0f);
+                    stgN[k] = v[j].y;
                 } else {
                     stg[s + TK * grp] = v[j];
                 }
@@ -829,16 +857,17 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
         if (packed) {
             // column 0: bins fy <= N/2 in prev[0..4]; the rest is the Hermitian
             // mirror (bitwise: F0[N-fy] = conj F0[fy] by the unpack formula).
-            // Column N/2 (stN) is mirrored the same way (rows fy <= N/2 were
-            // written by this same thread in the frame loop).
+            // Column N/2 (from ldsN, rows fy <= N/2 written by this same
+            // thread) is mirrored the same way.
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 const int fy = t0 + j * T;
                 if (j < 4 || fy == N / 2) {
                     state_out[fy] = prev[j];
+                    const c2 n = ldsN[fy];
+                    stN[fy] = n;
                     if (fy != 0 && fy != N / 2) {
                         state_out[N - fy] = mk(prev[j].x, -prev[j].y);
-                        const c2 n = stN[fy];
                         stN[N - fy] = mk(n.x, -n.y);
                     }
                 }
