@@ -4,8 +4,8 @@
 Workload (BASELINE.json configs[1]): a synthetic 1920x1080 RGBA8 stream,
 5-level pyramid, PhaseScale 25, pyramid mode with orientations = 1 (the
 reference's semantics).  One STEP = one pass of the hot path over one batch of
-`--frames-per-step` consecutive frames of the stream per GPU (default 30, so
-the default 10 timed steps are the 300-frame stream of the config).  Input
+`--frames-per-step` consecutive frames of the stream per GPU (default 100, so
+the default 3 timed steps are the 300-frame stream of the config).  Input
 frames are generated on the device and resident in HBM before timing.
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): the stream is
@@ -53,9 +53,9 @@ def compulsory_bytes(W, H, N, frames, b_in=4, b_out=4):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames-per-step", type=int, default=30)
+    ap.add_argument("--frames-per-step", type=int, default=100)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--levels", type=int, default=5)
