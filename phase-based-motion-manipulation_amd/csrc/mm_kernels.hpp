@@ -114,6 +114,18 @@ __device__ __forceinline__ int xcd_remap(int b, int nb)
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// Like xcd_remap, but each XCD owns runs of G consecutive blocks spread over the
+// whole range (run k on XCD k % 8): same-XCD neighbours still share L2 lines,
+// and work that varies smoothly with the block index is balanced over XCDs.
+// Falls back to xcd_remap when nb is not a multiple of 8 G.
+template <int G>
+__device__ __forceinline__ int xcd_interleave(int b, int nb)
+{
+    if (nb % (8 * G) != 0) return xcd_remap(b, nb);
+    const int x = b % 8, q = b / 8;
+    return ((q / G) * 8 + x) * G + q % G;
+}
+
 // Access at a 32-bit BYTE offset from a (workgroup-uniform) base: matches the
 // scalar-base + 32-bit vector-offset form of global loads/stores (an index
 // scaled as zext(i) * sizeof(T) needs 64-bit address math per access).
@@ -983,7 +995,13 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
 // rows [i0-1, i0+TR] x columns [c0-1, c0+TC]: their I/Q are staged once in LDS;
 // the horizontal 3-tap combine of every staged row and the TR+4 Yh values of the
 // thread's column then live in registers.  One barrier per tile.
-constexpr int kTileRows = 8, kTileCols = 256;
+#ifndef MM_K4_ROWS
+#define MM_K4_ROWS 8
+#endif
+#ifndef MM_K4_COLS
+#define MM_K4_COLS 256
+#endif
+constexpr int kTileRows = MM_K4_ROWS, kTileCols = MM_K4_COLS;
 
 template <int FMT>
 __global__ __launch_bounds__(kTileCols)

@@ -110,7 +110,12 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
     const int t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    // columns near kx = 0 and N carry more bands than those near N/2
+    // (band_col_zero): interleave column runs over the XCDs
+#ifndef MM_SB_COLS_RUN
+#define MM_SB_COLS_RUN 8
+#endif
+    const int blk = xcd_interleave<MM_SB_COLS_RUN>(blockIdx.x, gridDim.x);
     const int kx_raw = blk * GPW + grp;
     const bool valid = kx_raw < N;               // small N: more groups than columns
     const int kx = valid ? kx_raw : N - 1;
