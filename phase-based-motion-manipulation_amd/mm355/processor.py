@@ -6,8 +6,8 @@ snake_case; methods keep the reference's Unity callback names.
 """
 import numpy as np
 
-from .binding import (EDGE_REPEAT, MODE_PYRAMID, MODE_STANDARD, RGBA8, RGBA32F, Handle,
-                      MMError, Params)
+from .binding import (EDGE_REPEAT, FILTER_DIFF, MODE_PYRAMID, MODE_STANDARD, MODE_STEERABLE,
+                      RGBA8, RGBA32F, Handle, MMError, Params)
 
 
 def _fmt_of(frame):
@@ -36,7 +36,8 @@ class MotionMagnificationProcessor:
                  phase_scale=10.0, magnitude_threshold=0.01, apply_bandpass_filter=True,
                  low_frequency_cutoff=0.05, high_frequency_cutoff=0.4, filter_steepness=3.0,
                  motion_sensitivity=1.5, enhance_edges=True, edge_enhancement=0.8,
-                 edge_mode=EDGE_REPEAT, device=0):
+                 edge_mode=EDGE_REPEAT, orientations=1, temporal_filter=FILTER_DIFF,
+                 iir_low=None, iir_high=None, device=0):
         self.width, self.height, self.device = width, height, device
         self.apply_motion_magnification = apply_motion_magnification  # .cs:12
         self.show_magnitude = show_magnitude                          # .cs:13
@@ -55,6 +56,12 @@ class MotionMagnificationProcessor:
         self.enhance_edges = enhance_edges                            # .cs:42
         self.edge_enhancement = edge_enhancement                      # .cs:43
         self.edge_mode = edge_mode
+        # steerable extension (no reference counterpart):
+        # orientations 4/6/8 with the pyramid switch on select MM_MODE_STEERABLE;
+        # iir_low/iir_high None keep mm_params_default's coefficients
+        self.orientations = orientations
+        self.temporal_filter = temporal_filter
+        self.iir_low, self.iir_high = iir_low, iir_high
         self._handle = None
 
     # -- reference lifecycle -------------------------------------------------
@@ -62,6 +69,14 @@ class MotionMagnificationProcessor:
         # usePyramidDecomposition selects ProcessFrameWithPyramidDecomposition or
         # ProcessFrameWithStandardMagnification (.cs:128-135)
         mode = MODE_PYRAMID if self.use_pyramid_decomposition else MODE_STANDARD
+        steer = {}
+        if self.use_pyramid_decomposition and self.orientations != 1:
+            mode = MODE_STEERABLE
+            steer = dict(orientations=self.orientations, temporal_filter=self.temporal_filter)
+            if self.iir_low is not None:
+                steer["iir_low"] = self.iir_low
+            if self.iir_high is not None:
+                steer["iir_high"] = self.iir_high
         return Params.make(levels=self.pyramid_levels, min_freq=self.min_frequency,
                            max_freq=self.max_frequency, phase_scale=self.phase_scale,
                            magnitude_threshold=self.magnitude_threshold,
@@ -75,7 +90,8 @@ class MotionMagnificationProcessor:
                            enhance_edges=self.enhance_edges,
                            edge_enhancement=self.edge_enhancement,
                            # showMagnitude / showPhase: ProcessDebugView (.cs:119-123)
-                           show_magnitude=self.show_magnitude, show_phase=self.show_phase)
+                           show_magnitude=self.show_magnitude, show_phase=self.show_phase,
+                           **steer)
 
     def Start(self):
         """Start -> InitializeProcessor (.cs:90-94, :289-342). Raises on failure."""

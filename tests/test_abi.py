@@ -79,3 +79,19 @@ def test_resample_table_matches_oracle_pad(W, H, edge):
     got = ry[:, None] * rx[None, :]
     ref = canvas[y0:y0 + H, x0:x0 + W, 0]      # luma of gray = value
     assert np.abs(got - ref).max() < 2e-6
+
+
+def test_processor_params_mirror_inspector_fields():
+    """MotionMagnificationProcessor fields -> mm_params (host only, no handle)."""
+    P = mm355.MotionMagnificationProcessor
+    p = P(64, 48, pyramid_levels=4, phase_scale=25.0)._params()
+    assert (p.mode, p.levels, p.orientations) == (mm355.MODE_PYRAMID, 4, 1)
+    assert abs(p.phase_scale - 25.0) < 1e-6
+    assert P(64, 48, use_pyramid_decomposition=False)._params().mode == mm355.MODE_STANDARD
+    d = mm355.Params.make()
+    s = P(64, 48, orientations=8)._params()
+    assert (s.mode, s.orientations, s.temporal_filter) == (mm355.MODE_STEERABLE, 8, mm355.FILTER_DIFF)
+    assert (s.iir_low, s.iir_high) == (d.iir_low, d.iir_high)
+    s = P(64, 48, orientations=4, temporal_filter=mm355.FILTER_IIR, iir_low=0.1, iir_high=0.5)._params()
+    assert (s.mode, s.orientations, s.temporal_filter) == (mm355.MODE_STEERABLE, 4, mm355.FILTER_IIR)
+    assert abs(s.iir_low - 0.1) < 1e-7 and abs(s.iir_high - 0.5) < 1e-7
