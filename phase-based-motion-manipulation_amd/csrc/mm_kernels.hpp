@@ -609,9 +609,9 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 // the op runs on fy <= N/2 for both and the upper half is mirrored, through the
 // exchange buffer: the upper half of Z is stored for the partner reads
 // Z[N - fy], and the mirrored A goes into the (unused) lower half.  The
-// grid is then exactly N/2 groups (1024 at N=2048: one resident round at 4
-// WGs/CU instead of 1025 with a one-WG tail).  Column N/2's F_{t-1} lives in the
-// state buffer between frames.
+// grid is then exactly N/2 groups (512 two-column workgroups at N=2048: one
+// resident round at 2 WGs/CU, no one-group tail).  Column N/2's F_{t-1} stays
+// in LDS (ldsN) across the frames of a launch.
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
