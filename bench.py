@@ -75,6 +75,9 @@ def parse():
                     help="rehearsal: print per-frame output checksums (all ranks, rank 0) "
                          "instead of the bench line; sharded and single-rank runs of the "
                          "same frames must agree bitwise")
+    ap.add_argument("--replica-index", type=int, default=None,
+                    help="--mode replicas: which replica's stream this process runs "
+                         "(default: its RANK; seed = base + index)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="bound on the CPU-baseline sample")
@@ -183,6 +186,7 @@ def parity_check(mm355, torch, params, W, H, ref, local):
     import numpy as np
     n = ref.shape[0]
     h = mm355.Handle(W, H, params, device=local)
+    h.set_batch(n)
     fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
     out = torch.empty_like(fr)
     st = torch.cuda.current_stream().cuda_stream
@@ -220,8 +224,10 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     W, H, C = a.width, a.height, a.frames_per_step
-    os.environ.setdefault("MM_CHUNK", str(C))
     steer = a.orientations > 1
+    if steer and a.temporal_filter == "iir" and a.mode == "ring" and world > 1:
+        # the IIR state is a history of frames: mm_compute_state refuses it
+        raise SystemExit("--temporal-filter iir cannot be frame-sharded: use --mode replicas")
     if steer:
         params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
                                    mode=mm355.MODE_STEERABLE, orientations=a.orientations,
@@ -230,12 +236,14 @@ def main():
         params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
                                    mode=mm355.MODE_STANDARD if a.standard else mm355.MODE_PYRAMID)
     h = mm355.Handle(W, H, params, device=dev)
+    h.set_batch(C)      # one step = one batch: K2 keeps F_{t-1} on chip across it
     N = h.N
 
     # resident inputs: one buffer per step (warmup + timed), generated on device
     total_steps = a.warmup + a.steps
     ring = a.mode == "ring" and world > 1
-    seed = 0x5EED0000 + (0 if a.mode == "ring" else rank)
+    replica = rank if a.replica_index is None else a.replica_index
+    seed = 0x5EED0000 + (0 if a.mode == "ring" else replica)
     frames = torch.empty((total_steps, C, H, W, 4), dtype=torch.uint8, device="cuda")
     for s in range(total_steps):
         t0 = (s * world * C + rank * C) if a.mode == "ring" else s * C
@@ -270,11 +278,21 @@ def main():
     stream.finish()
     if a.checksum:
         sums = backend.sums
-        if world > 1:
+        if world > 1 and a.mode == "ring":
             allv = [None] * world
             dist.all_gather_object(allv, sums)
             sums = {k: v for d in allv for k, v in d.items()}
-        if rank == 0:
+        if a.mode == "replicas":   # every rank's own stream, keyed by rank
+            mine = [sums[k] for k in sorted(sums)]
+            allv = [None] * world
+            if world > 1:
+                dist.all_gather_object(allv, mine)
+            else:
+                allv = [mine]
+            if rank == 0:
+                print(json.dumps({"checksums_by_rank": {str(r): v for r, v in enumerate(allv)},
+                                  "world": world}), flush=True)
+        elif rank == 0:
             print(json.dumps({"checksums": [sums[k] for k in sorted(sums)],
                               "frames": sorted(sums)[:1] + sorted(sums)[-1:], "world": world}),
                   flush=True)

@@ -21,6 +21,8 @@
  *     (alpha included) and becomes the temporal state (.cs:111-117); after
  *     that output alpha is 1 (CombineYIQChannels.shader:56).
  *   - W and H must be even, max(W,H) <= 4096 (padded square N = nextpow2).
+ *   - Every entry point that takes a handle runs on the handle's device and
+ *     restores the caller's current HIP device before it returns.
  */
 #ifndef MM_H
 #define MM_H
@@ -31,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 4
+#define MM_ABI_VERSION 5
 
 /* error codes */
 #define MM_OK               0
@@ -135,7 +137,10 @@ int mm_reset(mm_handle *h);
 
 /* The temporal state carried between frames: the previous frame's spectrum
  * (what previousSourceTexture, .cs:142, is used for).  `dev_buf` is device
- * memory of mm_state_size() bytes.  Ordered on hip_stream (NULL = default stream). */
+ * memory of mm_state_size() bytes.  Ordered on hip_stream (NULL = default stream).
+ * MM_MODE_STEERABLE: the per-coefficient local phases (one float plane per
+ * band; MM_FILTER_IIR adds the two filter planes), so the size follows the
+ * mode, levels, orientations and filter of the current parameters. */
 int mm_state_size(const mm_handle *h, size_t *bytes);
 int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream);
 int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stream);
@@ -147,6 +152,16 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
 
 /* The handle's HIP stream (hipStream_t). */
 void *mm_stream(mm_handle *h);
+
+/* Frames per internal batch of mm_process_stream: the launches of one batch
+ * cover `frames` frames, and the column kernel keeps the previous spectrum on
+ * chip across them (its state is read and written once per batch).  Larger
+ * batches amortise that and the launch gaps; the hand-off buffers take about
+ * 26 MB per 1080p frame (4x at 2160p).  Default: min(64, 1 GiB of buffers).
+ * Results do not depend on the batch size.  Reallocates (synchronises the
+ * device); call between frames.  Since ABI 5. */
+int mm_set_batch(mm_handle *h, int frames);
+int mm_get_batch(const mm_handle *h, int *frames);
 
 /* OnDestroy/ReleaseResources (.cs:96-99, :344-356). */
 void mm_destroy(mm_handle *h);

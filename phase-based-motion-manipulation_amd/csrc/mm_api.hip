@@ -19,7 +19,6 @@
 #include <vector>
 
 #include "../../include/mm.h"
-#include "mm_kernels_w.hpp"
 #include "mm_steer.hpp"
 
 using namespace mm;
@@ -52,13 +51,12 @@ struct mm_handle {
     c2 *d_T;                    // band rows [nb+1][Hq][N] (row-major, k_sb_cols -> k_sb_rows)
     float *d_sst;               // temporal-filter state: phi, u_h, u_l planes [nb][Hn][W+4]
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
+    int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
     bool steer_valid;           // d_sst holds the state after the previous frame
     c2 *d_G, *d_Q, *d_state;
     float *d_Yh;
     size_t g_stride, q_stride, yh_stride;  // elements per frame
-    int chunk;                  // frames per K1/K2/K3 batch
-    int nsub;                   // K2 (wave form): sub-chunks per column and launch
-    bool k2_wave;               // K2 as one wave per column (k_cols_w), N = 512..2048
+    int chunk;                  // frames per K1/K2/K3 batch (mm_set_batch)
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
@@ -68,6 +66,27 @@ struct mm_handle {
     bool prof;
     std::vector<ProfRec> prof_recs;
 };
+
+// Makes the handle's device current for the scope of an entry point and gives
+// the caller's current device back on the way out (a multi-GPU host or an
+// engine plugin keeps its own device selection across mm_* calls).
+struct DeviceScope {
+    int prev = -1;
+    hipError_t err;
+    explicit DeviceScope(int dev)
+    {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+        else if (err == hipSuccess) prev = -1;   // already current: nothing to restore
+    }
+    ~DeviceScope()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+#define DEVICE_SCOPE(h)                                  \
+    DeviceScope dev_scope_((h)->device);                 \
+    if (dev_scope_.err != hipSuccess) return MM_ERR_HIP
 
 // Brackets one kernel launch with events when profiling is on.
 struct ProfScope {
@@ -290,33 +309,18 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
 
 template <int LOG2N>
 static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 *st_in,
-                     c2 *st_out, hipStream_t s)
+                     c2 *st_out, hipStream_t s, int g_frame = 0)
 {
     const int gpw = k2_groups<LOG2N>();
     const int cols = (1 << LOG2N) / 2;   // f = 0 and f = N/2 share group 0 (k_cols)
     const int blocks = (cols + gpw - 1) / gpw;
     ProfScope ps(h, s, MM_K_COLS, nframes);
-    if constexpr (LOG2N >= 9 && LOG2N <= 11) {
-        if (h->k2_wave) {
-            const int nsub = std::max(1, std::min(h->nsub, nframes));
-            const dim3 grid((1 << LOG2N) / 2 * nsub);
-            if (h->spec.mode == MM_MODE_STANDARD)
-                hipLaunchKernelGGL((k_cols_w<LOG2N, MM_MODE_STANDARD>), grid, dim3(64), 0, s,
-                                   h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out,
-                                   nframes, first_passthrough, nsub, h->geo, h->spec, h->d_tw);
-            else
-                hipLaunchKernelGGL((k_cols_w<LOG2N, MM_MODE_PYRAMID>), grid, dim3(64), 0, s,
-                                   h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out,
-                                   nframes, first_passthrough, nsub, h->geo, h->spec, h->d_tw);
-            HIPCHK(hipGetLastError());
-            return MM_OK;
-        }
-    }
     // per group: FFT exchange buffer + two per-bin tables (k_cols)
     const size_t lds = k2_lds_bytes<LOG2N>();
 #define MM_K2_LAUNCH(MODE)                                                                 \
     hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, \
-                       h->d_G, h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes,       \
+                       h->d_G + h->g_stride * g_frame, h->g_stride, h->d_Q, h->q_stride, st_in, \
+                       st_out, nframes,                                                         \
                        first_passthrough, h->geo, h->spec, h->d_tw)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
     else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB);
@@ -376,14 +380,20 @@ static int steer_bands(const mm_handle *h)
     const int nmid = h->spec.L >= 3 ? h->spec.L - 2 : 0;
     return nmid * (h->spec.O / 2);
 }
+// state planes: phi (DIFF reads only the previous local phase), + u_h, u_l (IIR)
+static int steer_planes(const mm_handle *h) { return h->spec.filt == MM_FILTER_IIR ? 3 : 1; }
+static size_t steer_plane_floats(const mm_handle *h)
+{
+    return (size_t)steer_bands(h) * h->geo.Hn * (h->W + 4);
+}
 static size_t steer_state_bytes(const mm_handle *h)
 {
-    return sizeof(float) * 3 * (size_t)steer_bands(h) * h->geo.Hn * (h->W + 4);
+    return sizeof(float) * steer_planes(h) * steer_plane_floats(h);
 }
 static int steer_alloc(mm_handle *h)
 {
     const int nb = steer_bands(h);
-    if (h->steer_nb == nb) return MM_OK;
+    if (h->steer_nb == nb && h->steer_planes >= steer_planes(h)) return MM_OK;
     (void)hipFree(h->d_Fb);
     (void)hipFree(h->d_T);
     (void)hipFree(h->d_sst);
@@ -397,6 +407,7 @@ static int steer_alloc(mm_handle *h)
         hipMalloc(&h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
+    h->steer_planes = steer_planes(h);
     return MM_OK;
 }
 
@@ -426,7 +437,9 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         HIPCHK(hipGetLastError());
     }
     const size_t band_stride = (size_t)N * h->geo.Hq;
-    const size_t plane = (size_t)steer_bands(h) * h->geo.Hn * (h->W + 4);
+    // DIFF reads and writes only the phi plane (a caller's DIFF state buffer
+    // holds just that plane); IIR the three
+    const size_t plane = steer_planes(h) == 3 ? steer_plane_floats(h) : 0;
     for (int k = 0; k < n; ++k) {
         const int reset = k < seed;
         {
@@ -445,6 +458,13 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         HIPCHK(hipGetLastError());
     }
     if (sst == h->d_sst) h->steer_valid = true;
+    // the frame spectrum state follows the input in this mode too (.cs:142), so
+    // that a switch back to the pyramid or standard mode magnifies against the
+    // last input: K2 in passthrough on the chunk's last K1 spectrum
+    if (sst == h->d_sst) {
+        if ((rc = launch_k2<LOG2N>(h, 1, 1, nullptr, h->d_state, s, n - 1))) return rc;
+        h->has_state = true;
+    }
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     if (!write) {
         if (out) HIPCHK(hipMemcpyAsync(out, in, fb * n, hipMemcpyDeviceToDevice, s));
@@ -688,6 +708,34 @@ static void free_handle(mm_handle *h)
     delete h;
 }
 
+// Frames per K1/K2/K3 batch by default: the hand-off buffers of a batch take
+// about 26 MB per 1080p frame; 1 GiB of them keeps K2's per-launch state load
+// and store (one per batch) small against the batch's work.
+static int default_batch(int W, int H, int N)
+{
+    const size_t per_frame = sizeof(c2) * ((size_t)(N / 2 + 1) * H + (size_t)(N / 2 + 2) * (H + 8)) +
+                             sizeof(float) * (size_t)(H + 4) * W;
+    return (int)std::max<size_t>(1, std::min<size_t>(64, ((size_t)1 << 30) / per_frame));
+}
+
+// (Re)allocates the per-batch hand-off buffers G, Q, Yh for `frames` frames.
+static int alloc_batch(mm_handle *h, int frames)
+{
+    (void)hipFree(h->d_G);
+    (void)hipFree(h->d_Q);
+    (void)hipFree(h->d_Yh);
+    (void)hipFree(h->d_Fb);   // steerable per-batch spectra: re-sized on next use
+    h->d_G = h->d_Q = h->d_Fb = nullptr;
+    h->d_Yh = nullptr;
+    h->steer_nb = -1;
+    if (hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * frames) != hipSuccess ||
+        hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * frames) != hipSuccess ||
+        hipMalloc(&h->d_Yh, sizeof(float) * h->yh_stride * frames) != hipSuccess)
+        return MM_ERR_OOM;
+    h->chunk = frames;
+    return MM_OK;
+}
+
 static bool taps_local(const std::vector<Tap4> &tab)
 {
     for (size_t i = 0; i < tab.size(); ++i)
@@ -745,7 +793,8 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) return MM_ERR_NO_DEVICE;
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MM_ERR_NO_DEVICE;
-    HIPCHK(hipSetDevice(hip_device));
+    DeviceScope dev_scope_(hip_device);
+    if (dev_scope_.err != hipSuccess) return MM_ERR_HIP;
 
     mm_handle *h = new (std::nothrow) mm_handle();
     if (!h) return MM_ERR_OOM;
@@ -772,14 +821,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->blur = build_blur();
 
-    const char *ch = getenv("MM_CHUNK");
-    h->chunk = ch ? std::max(1, atoi(ch)) : (N >= 4096 ? 4 : 8);
-    const char *ns = getenv("MM_NSUB");
-    h->nsub = ns ? std::max(1, atoi(ns)) : 3;
-    // K2 form: workgroup-per-column k_cols (default; fastest measured) or
-    // wave-per-column k_cols_w (MM_K2=wave; parity-tested)
-    const char *k2 = getenv("MM_K2");
-    h->k2_wave = k2 && strcmp(k2, "wave") == 0;
+    h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * height;
     h->q_stride = (size_t)g.Qs * g.Hq;
     h->yh_stride = (size_t)g.Hn * width;
@@ -793,9 +835,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
               hipMalloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
               hipMalloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
               hipMalloc(&h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
-              hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * h->chunk) == hipSuccess &&
-              hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * h->chunk) == hipSuccess &&
-              hipMalloc(&h->d_Yh, sizeof(float) * h->yh_stride * h->chunk) == hipSuccess &&
+              alloc_batch(h, h->chunk) == MM_OK &&
               hipMalloc(&h->d_state, sizeof(c2) * (size_t)(N / 2 + 1) * N) == hipSuccess;
     if (!ok) {
         free_handle(h);
@@ -820,6 +860,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->has_state = false;
     h->steer_nb = -1;
     h->steer_valid = false;
+    h->steer_planes = 0;
     if (getenv("MM_DEBUG"))
         fprintf(stderr, "mm355: Original: %dx%d, Padded: %dx%d\n", width, height, N, N);  // .cs:304
     *out = h;
@@ -832,12 +873,14 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     int rc = validate_params(p);
     if (rc) return rc;
     const bool edge_changed = p->edge_mode != h->p.edge_mode;
+    DEVICE_SCOPE(h);
     HIPCHK(hipDeviceSynchronize());   // in-flight work on any stream may read the tables
     const mm_params &o = h->p;
     if (p->mode != o.mode || p->levels != o.levels || p->orientations != o.orientations ||
         p->temporal_filter != o.temporal_filter || p->min_freq != o.min_freq ||
-        p->max_freq != o.max_freq || p->edge_mode != o.edge_mode)
-        h->steer_valid = false;   // local-phase state of other bands / masks
+        p->max_freq != o.max_freq || p->edge_mode != o.edge_mode || p->iir_low != o.iir_low ||
+        p->iir_high != o.iir_high)
+        h->steer_valid = false;   // local-phase state of other bands / masks / filter
     h->p = *p;
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
@@ -862,6 +905,22 @@ int mm_padded_size(const mm_handle *h, int *n)
 
 void *mm_stream(mm_handle *h) { return h ? (void *)h->stream : nullptr; }
 
+int mm_set_batch(mm_handle *h, int frames)
+{
+    if (!h || frames < 1 || frames > 4096) return MM_ERR_INVALID;
+    if (frames == h->chunk) return MM_OK;
+    DEVICE_SCOPE(h);
+    HIPCHK(hipDeviceSynchronize());   // in-flight batches use the buffers
+    return alloc_batch(h, frames);
+}
+
+int mm_get_batch(const mm_handle *h, int *frames)
+{
+    if (!h || !frames) return MM_ERR_INVALID;
+    *frames = h->chunk;
+    return MM_OK;
+}
+
 int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int format,
                       void *hip_stream)
 {
@@ -869,7 +928,7 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
     if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
     if (count == 0) return MM_OK;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
-    HIPCHK(hipSetDevice(h->device));
+    DEVICE_SCOPE(h);
     return do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
 }
 
@@ -880,7 +939,7 @@ int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, v
     if (flags & MM_FRAMES_ON_DEVICE) return mm_process_stream(h, in, out, 1, format, hip_stream);
     // host frames: stage through device buffers and synchronise
     const size_t fb = (size_t)h->W * h->H * (format ? 16 : 4);
-    HIPCHK(hipSetDevice(h->device));
+    DEVICE_SCOPE(h);
     if (h->stage_bytes < fb) {
         (void)hipFree(h->d_stage_in);
         (void)hipFree(h->d_stage_out);
@@ -921,6 +980,7 @@ int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     if (!h->has_state) return MM_ERR_NO_STATE;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
+    DEVICE_SCOPE(h);
     if (h->p.mode == MM_MODE_STEERABLE) {
         if (!h->steer_valid) return MM_ERR_NO_STATE;
         HIPCHK(hipMemcpyAsync(dev_buf, h->d_sst, need, hipMemcpyDeviceToDevice, s));
@@ -935,6 +995,7 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
     size_t need = 0;
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
+    DEVICE_SCOPE(h);
     if (h->p.mode == MM_MODE_STEERABLE) {
         int rc = steer_alloc(h);
         if (rc) return rc;
@@ -955,7 +1016,7 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
     if (!h || !in_dev || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
-    HIPCHK(hipSetDevice(h->device));
+    DEVICE_SCOPE(h);
     // the IIR state is a history of frames, not a function of one input frame
     if (h->p.mode == MM_MODE_STEERABLE && h->p.temporal_filter == MM_FILTER_IIR)
         return MM_ERR_UNSUPPORTED;
@@ -965,7 +1026,7 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
 void mm_destroy(mm_handle *h)
 {
     if (!h) return;
-    (void)hipSetDevice(h->device);
+    DeviceScope dev_scope_(h->device);
     (void)hipDeviceSynchronize();   // work on caller streams may still use the buffers
     free_handle(h);
 }

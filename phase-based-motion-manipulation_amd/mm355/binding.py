@@ -74,7 +74,7 @@ class Params(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 4   # include/mm.h MM_ABI_VERSION
+ABI_VERSION = 5   # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):
@@ -105,6 +105,8 @@ def load_library(path=None):
         "mm_set_state": (ci, [vp, vp, sz, vp]),
         "mm_compute_state": (ci, [vp, vp, ci, vp, sz, vp]),
         "mm_stream": (vp, [vp]),
+        "mm_set_batch": (ci, [vp, ci]),
+        "mm_get_batch": (ci, [vp, ctypes.POINTER(ci)]),
         "mm_destroy": (None, [vp]),
         "mm_synth_frames": (ci, [vp, ci, ci, ci, ci, ctypes.c_uint64, ci, vp]),
         "mm_resample_table": (ci, [ci, ci, ci, ci, ctypes.POINTER(ctypes.c_int32),
@@ -113,13 +115,15 @@ def load_library(path=None):
         "mm_profile_end": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci),
                                 ctypes.POINTER(ci)]),
     }
+    abi = L.mm_abi_version()
     for name, (res, args) in sigs.items():
+        if abi < 5 and name in ("mm_set_batch", "mm_get_batch"):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
     # mm_params grows only at its end: an older library (ABI >= 2) reads a prefix
     # of Params (A/B builds); a newer one than this binding is refused.
-    abi = L.mm_abi_version()
     if abi > ABI_VERSION or abi < 2:
         raise MMError(-1, f"{path}: ABI {abi}, binding expects <= {ABI_VERSION}")
     _lib = L
@@ -183,9 +187,23 @@ class Handle:
         n = ctypes.c_int()
         check(lib().mm_padded_size(self.h, ctypes.byref(n)), "mm_padded_size")
         self.N = n.value
+
+    @property
+    def state_bytes(self):
+        """mm_state_size: follows the current parameters (the steerable mode's
+        state depends on levels, orientations and temporal filter)."""
         s = ctypes.c_size_t()
         check(lib().mm_state_size(self.h, ctypes.byref(s)), "mm_state_size")
-        self.state_bytes = s.value
+        return s.value
+
+    def set_batch(self, frames):
+        check(lib().mm_set_batch(self.h, int(frames)), "mm_set_batch")
+
+    @property
+    def batch(self):
+        n = ctypes.c_int()
+        check(lib().mm_get_batch(self.h, ctypes.byref(n)), "mm_get_batch")
+        return n.value
 
     def close(self):
         if getattr(self, "h", None):

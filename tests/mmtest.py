@@ -40,7 +40,9 @@ def oracle_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, app
 
 
 def gpu_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, mode="frame",
-            apply=True, standard=None, debug=None):
+            apply=True, standard=None, debug=None, batch=8):
+    """batch: mm_set_batch frames per internal batch (8: multi-frame streams
+    cross batch boundaries, where K2's state is stored and reloaded)."""
     import torch
     import mm355
     extra = {} if standard is None else dict(mode=mm355.MODE_STANDARD, **_std_fields(standard))
@@ -49,6 +51,7 @@ def gpu_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, mode="
     p = mm355.Params.make(levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
                           edge_mode=edge, apply_magnification=apply, **extra)
     h = mm355.Handle(W, H, p)
+    h.set_batch(batch)
     fmt = mm355.RGBA8 if frames[0].dtype == np.uint8 else mm355.RGBA32F
     dev_in = torch.from_numpy(np.stack(frames)).cuda()
     dev_out = torch.empty_like(dev_in)

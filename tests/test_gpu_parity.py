@@ -49,7 +49,7 @@ def test_u8_frames():
 
 def test_stream_equals_per_frame_bitwise():
     W, H = 200, 120
-    fr = T.synth(W, H, 19)                  # crosses the 8-frame chunk boundary twice
+    fr = T.synth(W, H, 19)                  # crosses the 8-frame batch boundary twice
     a = T.gpu_run(W, H, fr, 5, 25.0, mode="frame")
     b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream")
     for x, y in zip(a, b):
@@ -354,6 +354,7 @@ def test_1080p_stream_device_synth_u8():
     import torch
     W, H, n = 1920, 1080, 10
     h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
+    h.set_batch(8)
     fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
     h.synth(fr, 0, n)
     out = torch.empty_like(fr)

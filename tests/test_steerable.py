@@ -60,13 +60,15 @@ def test_spec_static_scene_unchanged_by_diff():
 
 # ---- HIP path (GPU) -------------------------------------------------------------
 
-def gpu_steer(W, H, fr, levels=5, S=10.0, Oo=8, filt=0, rl=0.05, rh=0.4, edge=0, apply=True):
+def gpu_steer(W, H, fr, levels=5, S=10.0, Oo=8, filt=0, rl=0.05, rh=0.4, edge=0, apply=True,
+              batch=4):
     import mm355
     import torch
     p = mm355.Params.make(levels=levels, phase_scale=S, edge_mode=edge, apply_magnification=apply,
                           mode=mm355.MODE_STEERABLE, orientations=Oo, temporal_filter=filt,
                           iir_low=rl, iir_high=rh)
     h = mm355.Handle(W, H, p)
+    h.set_batch(batch)
     dev = torch.from_numpy(np.stack(fr)).cuda()
     out = torch.empty_like(dev)
     h.process_stream(dev, out, len(fr), mm355.RGBA32F)
@@ -112,7 +114,7 @@ def test_gpu_matches_spec(W, H, Oo, filt, S, edge):
 
 @pytest.mark.gpu
 def test_gpu_chunked_and_state_handoff():
-    """Chunk boundaries (MM_CHUNK 8 by default) and the DIFF state hand-off:
+    """Batch boundaries (mm_set_batch 4) and the DIFF state hand-off:
     a second handle seeded with mm_compute_state(frame k-1) continues the
     stream bitwise; mm_get_state/mm_set_state carry the IIR state."""
     import mm355
@@ -124,20 +126,24 @@ def test_gpu_chunked_and_state_handoff():
         p = mm355.Params.make(levels=5, phase_scale=10.0, mode=mm355.MODE_STEERABLE,
                               orientations=8, temporal_filter=filt)
         a = mm355.Handle(W, H, p)
+        a.set_batch(4)
         full = torch.empty_like(dev)
         a.process_stream(dev, full, n, mm355.RGBA32F)
         b = mm355.Handle(W, H, p)
+        b.set_batch(4)
         part = torch.empty_like(dev)
         b.process_stream(dev[:6], part[:6], 6, mm355.RGBA32F)
         st = torch.empty(b.state_bytes, dtype=torch.uint8, device="cuda")
         b.get_state(st)
         c = mm355.Handle(W, H, p)
+        c.set_batch(4)
         c.set_state(st)
         c.process_stream(dev[6:], part[6:], n - 6, mm355.RGBA32F)
         torch.cuda.synchronize()
         assert torch.equal(full, part), filt
         if filt == 0:
             d = mm355.Handle(W, H, p)
+            d.set_batch(4)
             st2 = torch.empty(d.state_bytes, dtype=torch.uint8, device="cuda")
             d.compute_state(dev[5], mm355.RGBA32F, st2)
             d.set_state(st2)
