@@ -27,9 +27,19 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "phase-based-motion-manipulation_amd"))
 
-METRIC = ("magnified frames/sec at 1920×1080, 5-level pyramid; "
-          "achieved HBM GB/s vs peak")
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def metric_name(W, H, L, orientations=1, standard=False):
+    """BASELINE.json's metric, naming the configuration actually run (the
+    default config reproduces BASELINE.json's string exactly)."""
+    if standard:
+        kind = "standard (non-pyramid) mode"
+    elif orientations > 1:
+        kind = f"{L}-level {orientations}-orientation steerable pyramid"
+    else:
+        kind = f"{L}-level pyramid"
+    return f"magnified frames/sec at {W}\u00d7{H}, {kind}; achieved HBM GB/s vs peak"
 
 
 def survey_bytes_per_frame(W, H, N, b_in=4, b_out=4):
@@ -81,14 +91,29 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="bound on the CPU-baseline sample")
+    ap.add_argument("--call-pattern", choices=("batch", "per-frame"), default="batch",
+                    help="per-frame: the reference's own call pattern (OnRenderImage once "
+                         "per frame, .cs:101-143): mm_process on device pointers, one frame "
+                         "per call, batch size 1 (N=1 only)")
+    ap.add_argument("--drop-in-frames", type=int, default=300,
+                    help="frames of the per-frame drop-in leg reported beside the batch "
+                         "rate (0: skip)")
+    # internal: CPU-baseline child process (cpu_baseline)
+    ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-out", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-threads", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-frames", type=int, default=30, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-keep", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
 class GpuBackend:
     """ShardedStream backend over one mm355 handle; frames pre-generated."""
 
-    def __init__(self, handle, frames, out, fmt, chunk, world, rank, torch, host_exchange=False):
+    def __init__(self, handle, frames, out, fmt, chunk, world, rank, torch, host_exchange=False,
+                 per_frame=False):
         self.h, self.frames, self.out, self.fmt = handle, frames, out, fmt
+        self.per_frame = per_frame    # --call-pattern per-frame: one mm_process per frame
         self.chunk, self.world, self.rank, self.torch = chunk, world, rank, torch
         self.host = host_exchange     # gloo rehearsal: exchanged states live on the host
         self.sums = None              # --checksum: global frame index -> byte sum
@@ -121,8 +146,14 @@ class GpuBackend:
 
     def process(self, lo, count):
         s, k = self._local(lo)
-        self.h.process_stream(self.frames[s % len(self.frames), k], self.out, count, self.fmt,
-                              stream=self._stream())
+        if self.per_frame:
+            src = self.frames[s % len(self.frames)]
+            for i in range(count):
+                self.h.process(src[k + i], self.out[i], self.fmt, on_device=True,
+                               stream=self._stream())
+        else:
+            self.h.process_stream(self.frames[s % len(self.frames), k], self.out, count, self.fmt,
+                                  stream=self._stream())
         if self.sums is not None:
             v = self.out[:count].reshape(count, -1).sum(dim=1, dtype=self.torch.int64).cpu()
             for i in range(count):
@@ -139,43 +170,94 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(W, H, L, S, seconds, standard=False):
-    """The CPU oracle (literal restatement of the reference algorithm) on the
-    host cores, bounded sample of the same stream (BASELINE.md CPU-baseline
-    plan: all-core and single-thread).  Returns (record, outputs) where
-    outputs are the oracle's RGBA8 frames 0..n, kept for the parity check."""
+def available_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2
+    CPU quota when one is set (a GPU box shows every host CPU in
+    os.cpu_count() but grants each job a share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _cpu_worker(a):
+    """Child process of cpu_baseline: times the oracle on `--cpu-threads`
+    threads (bound by OMP_PROC_BIND/OMP_PLACES from the parent's env, read when
+    libgomp loads) and writes its record (+ RGBA8 outputs) to --cpu-out."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_py as O
+    W, H, L, S = a.width, a.height, a.levels, a.phase_scale
+    thr = O.set_threads(a.cpu_threads)
+    o = O.Oracle(W, H, levels=L, phase_scale=S)
+    if a.standard:
+        o.set_standard(True)
+    outs = [o.process(O.synth_frame(W, H, 0))]    # passthrough, not timed
+    n, t0 = 0, time.perf_counter()
+    while n < a.cpu_frames:
+        y = o.process(O.synth_frame(W, H, n + 1))
+        if a.cpu_keep:
+            outs.append(y)
+        n += 1
+        if time.perf_counter() - t0 >= a.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    o.close()
+    if a.cpu_keep:
+        np.save(a.cpu_out + ".npy", np.stack(outs))
+    json.dump({"threads": thr, "frames": n, "seconds": dt}, open(a.cpu_out, "w"))
 
-    def run(threads, max_frames, budget, keep):
-        threads = O.set_threads(threads)
-        o = O.Oracle(W, H, levels=L, phase_scale=S)
-        if standard:
-            o.set_standard(True)
-        outs = [o.process(O.synth_frame(W, H, 0))]    # passthrough, not timed
-        n, t0 = 0, time.perf_counter()
-        while n < max_frames:
-            y = o.process(O.synth_frame(W, H, n + 1))
+
+def cpu_baseline(a):
+    """The CPU oracle (literal restatement of the reference algorithm: radix-2,
+    2 forward FFTs per frame, per-level passes) on a bounded sample of the same
+    stream, all-core (every CPU available to this job, threads bound with
+    OMP_PROC_BIND=close / OMP_PLACES=cores) and single-thread, each in its own
+    process so the OpenMP binding applies.  Returns (record, outputs): the
+    all-core run's RGBA8 frames 0..n feed the parity check."""
+    import subprocess
+    import tempfile
+    import numpy as np
+    W, H, L, S = a.width, a.height, a.levels, a.phase_scale
+    cores = available_cpus()
+
+    def run(threads, max_frames, seconds, keep):
+        with tempfile.TemporaryDirectory() as d:
+            out = os.path.join(d, "cpu.json")
+            env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close",
+                       OMP_PLACES="cores")
+            cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", "--cpu-out", out,
+                   "--cpu-threads", str(threads), "--cpu-frames", str(max_frames),
+                   "--cpu-seconds", str(seconds), "--width", str(W), "--height", str(H),
+                   "--levels", str(L), "--phase-scale", str(S)]
             if keep:
-                outs.append(y)
-            n += 1
-            if time.perf_counter() - t0 >= budget:
-                break
-        dt = time.perf_counter() - t0
-        o.close()
-        return threads, n, dt, (np.stack(outs) if keep else None)
+                cmd.append("--cpu-keep")
+            if a.standard:
+                cmd.append("--standard")
+            subprocess.run(cmd, env=env, check=True, timeout=seconds * 4 + 120)
+            rec = json.load(open(out))
+            outs = np.load(out + ".npy") if keep else None
+        return rec["threads"], rec["frames"], rec["seconds"], outs
 
-    all_threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
-    thr, n, dt, outs = run(all_threads, 30, seconds, True)
-    _, n1, dt1, _ = run(1, 30, seconds / 3, False)
+    thr, n, dt, outs = run(cores, 30, a.cpu_seconds, True)
+    _, n1, dt1, _ = run(1, 30, a.cpu_seconds / 3, False)
     rec = {"value": round(n / dt, 4), "unit": "frames/s", "cores": thr, "kind": "port",
            "single_thread_value": round(n1 / dt1, 4), "single_thread_frames": n1,
-           "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+           "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(), "cpus_available": cores,
+           "binding": "OMP_PROC_BIND=close OMP_PLACES=cores",
            "sample": f"{n} frames (t=1..{n}) of the same {W}x{H} synthetic RGBA8 stream "
                      f"(seed 0x5EED0000), L={L}, S={S}, after the passthrough frame; literal "
                      f"fp32 C restatement (radix-2, 2 forward FFTs/frame, per-level passes), "
-                     f"OpenMP {thr} threads; single-thread on t=1..{n1}"}
+                     f"OpenMP {thr} threads (every CPU available to this job: affinity mask "
+                     f"and cgroup quota; the host shows {os.cpu_count()}); single-thread on "
+                     f"t=1..{n1}"}
     return rec, outs
 
 
@@ -202,8 +284,72 @@ def parity_check(mm355, torch, params, W, H, ref, local):
             "bar": "max 1 LSB, <= 0.1% of values"}
 
 
+def drop_in_per_frame(mm355, torch, params, W, H, frames, local, count):
+    """The reference's call pattern (OnRenderImage once per frame,
+    .cs:101-143): a fresh handle at batch size 1, mm_process with device
+    pointers, one frame per call on one stream.  Every call pays K2's state
+    load + store and four launches.  Returns frames/s over the calls (after
+    the passthrough frame and 10 warm-up calls) and the HIP-event latency of
+    each call."""
+    h = mm355.Handle(W, H, params, device=local)
+    h.set_batch(1)
+    src = frames.reshape(-1, H, W, 4)
+    out = torch.empty((2, H, W, 4), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    sp = st.cuda_stream
+    warm = 11
+    count = min(count, src.shape[0] - warm)
+    for k in range(warm):
+        h.process(src[k], out[k & 1], mm355.RGBA8, on_device=True, stream=sp)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(count + 1)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record(st)
+    for k in range(count):
+        h.process(src[warm + k], out[k & 1], mm355.RGBA8, on_device=True, stream=sp)
+        ev[k + 1].record(st)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    h.close()
+    lat = sorted(ev[k].elapsed_time(ev[k + 1]) for k in range(count))
+    pick = lambda q: round(lat[min(count - 1, int(q * count))], 5)
+    return {"frames": count, "frames_per_s": round(count / wall, 2),
+            "latency_ms": {"mean": round(sum(lat) / count, 5), "p50": pick(0.5),
+                           "p99": pick(0.99), "max": round(lat[-1], 5)},
+            "pattern": "mm_process(MM_FRAMES_ON_DEVICE), batch 1, one call per frame "
+                       "(.cs:101-143 OnRenderImage); latency = HIP events around each call "
+                       "on its stream"}
+
+
+def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None):
+    """Frame-level HBM roofline: the design's compulsory bytes per output
+    frame (the four kernels' compulsory_bytes() at this batch size, per frame)
+    x frames/s per GPU vs 8 TB/s; PMC bytes per frame (profiles/traffic.json,
+    rocprofv3 FETCH_SIZE/WRITE_SIZE) beside them."""
+    cb = compulsory_bytes(W, H, N, batch)
+    per_frame = sum(cb.values()) / batch
+    rec = {"bytes_per_frame": int(per_frame),
+           "achieved_GBps": round(per_frame * fps_per_gpu / 1e9, 1),
+           "peak": HBM_PEAK_GBPS, "frac": round(per_frame * fps_per_gpu / 1e9 / HBM_PEAK_GBPS, 4),
+           "pmc_bytes_per_frame": None, "pmc_ratio": None,
+           "note": "compulsory bytes of K1+K2+K3+K4 per frame (DESIGN.md §5) x frames/s per GPU"}
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            pmc = sum(k["hbm_bytes_per_frame"] for k in tj["kernels"].values())
+            rec["pmc_bytes_per_frame"] = int(pmc)
+            rec["pmc_ratio"] = round(pmc / per_frame, 4)
+            rec["pmc_source"] = "profiles/traffic.json"
+        except Exception:
+            pass
+    return rec
+
+
 def main():
     a = parse()
+    if a.cpu_worker:
+        return _cpu_worker(a)
     import torch
     import torch.distributed as dist
     import mm355
@@ -236,7 +382,10 @@ def main():
         params = mm355.Params.make(levels=a.levels, phase_scale=a.phase_scale,
                                    mode=mm355.MODE_STANDARD if a.standard else mm355.MODE_PYRAMID)
     h = mm355.Handle(W, H, params, device=dev)
-    h.set_batch(C)      # one step = one batch: K2 keeps F_{t-1} on chip across it
+    per_frame = a.call_pattern == "per-frame"
+    # one step = one batch: K2 keeps F_{t-1} on chip across it; the per-frame
+    # pattern is the reference's one OnRenderImage per frame (batch 1)
+    h.set_batch(1 if per_frame else C)
     N = h.N
 
     # resident inputs: one buffer per step (warmup + timed), generated on device
@@ -250,7 +399,7 @@ def main():
         h.synth(frames[s], t0, C, seed=seed, stream=torch.cuda.current_stream().cuda_stream)
     out = torch.empty((C, H, W, 4), dtype=torch.uint8, device="cuda")
     backend = GpuBackend(h, frames, out, mm355.RGBA8, C, world if ring else 1,
-                         rank if ring else 0, torch, host_exchange=gloo)
+                         rank if ring else 0, torch, host_exchange=gloo, per_frame=per_frame)
     stream = ShardedStream(backend, C, rank if ring else 0, world if ring else 1)
     if a.checksum:
         backend.sums = {}
@@ -335,14 +484,16 @@ def main():
         try:
             vj = json.load(open(vfile))[dom]
             valu = {"valu_busy": vj["valu_busy"], "valu_insts_per_launch": vj["valu_insts_per_launch"],
-                    "source": "profiles/valu.json (rocprofv3 SQ_INSTS_VALU x 4 cycles / "
-                              "(1024 SIMDs x kernel cycles)); the FFT kernels are VALU-issue-bound"}
+                    "source": "profiles/valu.json: rocprofv3 SQ_INSTS_VALU x 4 cycles (measured "
+                              "issue cost of a wave64 VALU instruction, "
+                              "profiles/r02_valu_calib.json) / (1024 SIMDs x kernel cycles)"}
         except Exception:
             valu = None
     B = survey_bytes_per_frame(W, H, N)
+    batch = 1 if per_frame else C
 
     result = {
-        "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
+        "metric": metric_name(W, H, a.levels, a.orientations, a.standard), "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
@@ -354,6 +505,8 @@ def main():
                                 f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
                                 f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)"),
                    "frames_per_step_per_gpu": C, "padded_n": N,
+                   "call_pattern": ("one mm_process per frame (batch 1)" if per_frame else
+                                    f"mm_process_stream, batch {C} frames per call"),
                    "parallelism": (f"frame-sharded x{world}, "
                                    + ("gloo rehearsal, ring state via host" if gloo
                                       else "RCCL ring state shift")
@@ -365,17 +518,23 @@ def main():
                      "bytes_model": "compulsory bytes of the dominant kernel (DESIGN.md §5); "
                                     "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch",
                      "compute": valu},
+        "frame_roofline": (frame_roofline(W, H, N, fps / world, batch) if not steer else None),
         "survey_model": {"bytes_per_frame": B,
-                         "achieved_GBps_per_gpu": round(B * fps / world / 1e9, 1),
-                         "frac": round(B * fps / world / 1e9 / HBM_PEAK_GBPS, 4),
-                         "note": "SURVEY.md §8(d) B=W*H*(2b_in+b_out)+6*N^2*8; 100% = "
-                                 f"{HBM_PEAK_GBPS * 1e9 / B:.0f} frames/s per GPU"},
+                         "equivalent_GBps_per_gpu": round(B * fps / world / 1e9, 1),
+                         "note": "SURVEY.md §8(d) B=W*H*(2b_in+b_out)+6*N^2*8 charges dense "
+                                 "N x N hand-offs and a per-frame state round trip that this "
+                                 "design does not move; B x fps is an equivalent rate, not a "
+                                 "roofline fraction (it can exceed peak). The frame-level "
+                                 "fraction is frame_roofline.frac"},
         "kernels": kern,
     }
     h.close()
+    if world == 1 and not per_frame and a.drop_in_frames > 0 and not steer and not a.checksum:
+        # the reference's call pattern beside the batch rate (same frames)
+        result["drop_in_per_frame"] = drop_in_per_frame(mm355, torch, params, W, H, frames,
+                                                        local, a.drop_in_frames)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not steer:
-        result["cpu_baseline"], ref = cpu_baseline(W, H, a.levels, a.phase_scale,
-                                                   a.cpu_seconds, a.standard)
+        result["cpu_baseline"], ref = cpu_baseline(a)
         result["parity_vs_oracle"] = parity_check(mm355, torch, params, W, H, ref, local)
     if rank == 0:
         print(json.dumps(result), flush=True)

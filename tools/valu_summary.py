@@ -6,8 +6,14 @@ usage: valu_summary.py PMC_DIR[,PMC_DIR...] KERNEL_TRACE_DIR OUT_JSON
 valu_busy = SQ_INSTS_VALU * 4 cycles / (SIMDs * kernel cycles), with the
 kernel's cycles from its average kernel-trace duration and the shader clock
 derived from SQ_BUSY_CYCLES (summed over the shader engines) over that
-duration.  4 cycles = issue cost of one wave64 VALU instruction on a 16-lane
-SIMD (MI355X_MICROARCH.md, vector-instruction issue table).
+duration.  4 cycles = issue cost of one wave64 VALU instruction on gfx950,
+MEASURED by tools/valu_calib.hip (profiles/r02_valu_calib.json: v_fma_f32
+4.17, v_add_f32 4.29, v_pk_fma_f32 4.18 cycles per wave-instruction per SIMD at
+8 waves/SIMD, clock from s_memtime/s_memrealtime; v_sin_f32 8.2).  A 2-cycle
+cost would put the calibration kernels at 2x their measured time.
+valu_busy_peak_clk uses the 2.4 GHz peak clock instead (a lower bound: the
+clock under load is <= peak), since the SQ_BUSY_CYCLES clock estimate can
+undershoot and push valu_busy above 1.
 """
 import csv
 import glob
@@ -49,7 +55,8 @@ for k, c in pmc.items():
     out[k] = {"valu_insts_per_launch": valu, "salu_insts_per_launch": max(c.get("SQ_INSTS_SALU", [0])),
               "lds_insts_per_launch": max(c.get("SQ_INSTS_LDS", [0])),
               "launch_s": t, "clock_GHz": round(clk / 1e9, 3),
-              "valu_busy": round(valu * 4 / (SIMDS * clk * t), 3)}
+              "valu_busy": round(valu * 4 / (SIMDS * clk * t), 3),
+              "valu_busy_peak_clk": round(valu * 4 / (SIMDS * 2.4e9 * t), 3)}
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 for k, v in sorted(out.items()):
     print(k, v)
