@@ -6,5 +6,5 @@ tail -2 gpurun_out/test_$TAG.log
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo BENCH FAIL; tail gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > /dev/null 2> gpurun_out/prof_$TAG.err || { echo PROF FAIL; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --drop-in-frames 0 > /dev/null 2> gpurun_out/prof_$TAG.err || { echo PROF FAIL; exit 1; }
 cut -d, -f1-4 gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -c1-60,200-

@@ -3,7 +3,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; export TMPDIR=/tmp
 TAG=${1:-stall}; shift
-B="python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 $*"
+B="python3 $R/bench.py --no-cpu-baseline --drop-in-frames 0 --steps 2 --warmup 1 $*"
 i=0
 for CNT in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAVES SQ_INSTS_VMEM"; do
