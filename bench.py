@@ -474,8 +474,8 @@ def main():
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            per_frame = tj["kernels"][dom]["hbm_bytes_per_frame"]
-            traffic = round(per_frame * dk["frames"] / dk["launches"])
+            pmc_frame = tj["kernels"][dom]["hbm_bytes_per_frame"]
+            traffic = round(pmc_frame * dk["frames"] / dk["launches"])
         except Exception:
             traffic = None
     valu = None
@@ -507,7 +507,8 @@ def main():
                    "frames_per_step_per_gpu": C, "padded_n": N,
                    "call_pattern": ("one mm_process per frame (batch 1)" if per_frame else
                                     f"mm_process_stream, batch {C} frames per call"),
-                   "parallelism": (f"frame-sharded x{world}, "
+                   "parallelism": ("single GPU" if world == 1 else
+                                   f"frame-sharded x{world}, "
                                    + ("gloo rehearsal, ring state via host" if gloo
                                       else "RCCL ring state shift")
                                    if ring else f"replicas x{world}")},

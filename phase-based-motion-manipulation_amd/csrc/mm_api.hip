@@ -1080,4 +1080,13 @@ int mm_synth_frames(void *dev_out, int width, int height, int t0, int count, uin
     return MM_OK;
 }
 
+#ifdef MM_K2_STAMPS
+// diagnostic builds only (not in include/mm.h): k_cols phase cycle totals per wave
+int mm_debug_k2_stamps(unsigned long long *host, int n)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(mm_k2_stamps), sizeof(unsigned long long) * n) == hipSuccess
+               ? MM_OK : MM_ERR_HIP;
+}
+#endif
+
 }  // extern "C"

@@ -16,43 +16,72 @@
 
 namespace mm {
 
-// Complex value.  Scalar FP32 on purpose: as a 2-wide vector the complex math
-// lowers to v_pk_*_f32, which on gfx950 measured SLOWER per frame than the
-// scalar form in these VALU-issue-bound kernels (k_cols 15.5 vs 13.9 us/frame
-// with 19% fewer VALU instructions), besides costing registers.
-struct c2 { float x, y; };
+// Complex value: a 2 x f32 vector, so that it lives in an aligned VGPR pair
+// and the complex arithmetic issues as packed FP32 (VOP3P v_pk_add_f32 /
+// v_pk_mul_f32 / v_pk_fma_f32: two lanes' worth of f32 work per wave64
+// instruction at the issue cost of one scalar v_fma_f32 — 4.2 cycles per
+// wave-instruction either way, profiles/r02_valu_calib.json).  Plain sums and
+// differences use the vector operators (the compiler emits v_pk_add_f32 with
+// neg modifiers); products and the +-i rotations, whose operands must be
+// swizzled, are written as single VOP3P instructions with op_sel / neg
+// modifiers (the compiler's own lowering of those swizzles adds v_pk_mov and
+// negations).
+typedef float c2 __attribute__((ext_vector_type(2)));
 
-__host__ __device__ __forceinline__ c2 mk(float x, float y) { c2 r; r.x = x; r.y = y; return r; }
-__device__ __forceinline__ c2 add(c2 a, c2 b) { return mk(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ c2 sub(c2 a, c2 b) { return mk(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ c2 operator+(c2 a, c2 b) { return add(a, b); }
-__device__ __forceinline__ c2 operator-(c2 a, c2 b) { return sub(a, b); }
-__device__ __forceinline__ c2 operator*(c2 a, float s) { return mk(a.x * s, a.y * s); }
-// x + i*DIR*y and x - i*DIR*y
+__host__ __device__ __forceinline__ c2 mk(float x, float y) { c2 r = {x, y}; return r; }
+__device__ __forceinline__ c2 add(c2 a, c2 b) { return a + b; }
+__device__ __forceinline__ c2 sub(c2 a, c2 b) { return a - b; }
+__device__ __forceinline__ c2 scale(c2 a, float s) { return a * s; }
+
+// x + i*DIR*y: DIR = +1 -> (x.x - y.y, x.y + y.x); DIR = -1 -> (x.x + y.y, x.y - y.x)
 template <int DIR>
 __device__ __forceinline__ c2 add_i(c2 x, c2 y)
 {
-    return DIR < 0 ? mk(x.x + y.y, x.y - y.x) : mk(x.x - y.y, x.y + y.x);
+    c2 d;
+    if constexpr (DIR > 0)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(d) : "v"(x), "v"(y));
+    else
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(x), "v"(y));
+    return d;
 }
+// x - i*DIR*y
 template <int DIR>
-__device__ __forceinline__ c2 sub_i(c2 x, c2 y)
+__device__ __forceinline__ c2 sub_i(c2 x, c2 y) { return add_i<-DIR>(x, y); }
+
+// a * w = (ax wx - ay wy, ax wy + ay wx): t = (ax wx, ax wy), then
+// d = (-ay wy + t.x, ay wx + t.y)
+__device__ __forceinline__ c2 mul(c2 a, c2 w)
 {
-    return DIR < 0 ? mk(x.x - y.y, x.y + y.x) : mk(x.x + y.y, x.y - y.x);
+    c2 t, d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+        : "=v"(d) : "v"(a), "v"(w), "v"(t));
+    return d;
 }
-// multiply by i*DIR  (DIR = -1 forward -> -i ; DIR = +1 inverse -> +i)
+// a * w in plain C, for the spectral ops: their factors come straight from
+// transcendental instructions (v_sin/v_cos), and a transcendental result read
+// by the next instruction needs a wait state that the compiler inserts for
+// its own instructions but not in front of inline asm (an asm mul() there read
+// stale values on gfx950).  The FFT's asm operands come from loads and plain
+// VALU results only.
+__device__ __forceinline__ c2 mul_c(c2 a, c2 w)
+{
+    return mk(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+// a * conj(w) = (ax wx + ay wy, ay wx - ax wy): the inverse FFT's twiddles
+// from the forward bases without a conjugated copy
+__device__ __forceinline__ c2 mul_conj(c2 a, c2 w)
+{
+    c2 t, d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+        : "=v"(d) : "v"(a), "v"(w), "v"(t));
+    return d;
+}
+// a * w^DIR-convention: the forward (DIR < 0) FFT multiplies by the table's
+// W_N^k, the inverse by its conjugate
 template <int DIR>
-__device__ __forceinline__ c2 mul_i(c2 a)
-{
-    return DIR < 0 ? mk(a.y, -a.x) : mk(-a.y, a.x);
-}
-__device__ __forceinline__ c2 mul(c2 a, c2 b)
-{
-    return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-// the packed-form signature, kept for the shared butterfly code (wp unused)
-__device__ __forceinline__ c2 mul_p(c2 a, c2 w, c2) { return mul(a, w); }
-__device__ __forceinline__ c2 prime(c2 w) { return w; }
-__device__ __forceinline__ c2 scale(c2 a, float s) { return mk(a.x * s, a.y * s); }
+__device__ __forceinline__ c2 mul_tw(c2 a, c2 w) { return DIR < 0 ? mul(a, w) : mul_conj(a, w); }
 
 // LDS index padding: one complex every 8 (bank-conflict-free Stockham writes
 // for Ns = 1 and Ns = 8 with ds_write_b64).
@@ -86,10 +115,10 @@ __device__ __forceinline__ void dft8(c2 *v)
     c2 a1 = v[1] + v[5], b1 = v[1] - v[5];
     c2 a2 = v[2] + v[6], b2 = v[2] - v[6];
     c2 a3 = v[3] + v[7], b3 = v[3] - v[7];
-    // b[n] *= W8^n, W8 = exp(DIR*i*pi/4) = (h, DIR h); W8^2 = i*DIR folds into
-    // the DFT4 below, W8^3 = i*DIR*W8
-    b1 = mul_p(b1, c2{h, DIR * h}, c2{-DIR * h, h});
-    b3 = mul_p(b3, c2{-h, DIR * h}, c2{-DIR * h, -h});
+    // b[n] *= W8^n, W8 = exp(DIR*i*pi/4) = h (1 + i DIR); W8^2 = i*DIR folds into
+    // the DFT4 below, W8^3 = h (-1 + i DIR) = -h (b - i DIR b) / b
+    b1 = add_i<DIR>(b1, b1) * h;
+    b3 = sub_i<DIR>(b3, b3) * (-h);
     dft4<DIR>(a0, a1, a2, a3);
     // DFT4 of (b0, b1, i DIR b2, b3)
     const c2 s0 = add_i<DIR>(b0, b2), d0 = sub_i<DIR>(b0, b2);
@@ -101,48 +130,40 @@ __device__ __forceinline__ void dft8(c2 *v)
     v[7] = sub_i<DIR>(d0, t);
 }
 
-// u[m] *= w^m (m < R, R <= 16), powers by products of the base w (<= 4
-// roundings).  Every product and every multiply is mul_p (2 packed ops) with
-// the primed operand computed once.
-template <int R>
+// u[m] *= w^m (m < R, R <= 16) for the forward FFT (DIR < 0), u[m] *=
+// conj(w)^m for the inverse: w is always the forward base, its powers are
+// products (<= 4 roundings), and only the final multiply conjugates.
+template <int R, int DIR>
 __device__ __forceinline__ void apply_twiddles(c2 *u, c2 w1)
 {
-    const c2 p1 = prime(w1);
-    if constexpr (R >= 2) u[1] = mul_p(u[1], w1, p1);
+    if constexpr (R >= 2) u[1] = mul_tw<DIR>(u[1], w1);
     if constexpr (R >= 4) {
-        const c2 w2 = mul_p(w1, w1, p1), p2 = prime(w2);
-        const c2 w3 = mul_p(w2, w1, p1);
-        u[2] = mul_p(u[2], w2, p2);
-        u[3] = mul(u[3], w3);
+        const c2 w2 = mul(w1, w1);
+        const c2 w3 = mul(w2, w1);
+        u[2] = mul_tw<DIR>(u[2], w2);
+        u[3] = mul_tw<DIR>(u[3], w3);
         if constexpr (R >= 8) {
-            const c2 w4 = mul_p(w2, w2, p2), p4 = prime(w4);
-            u[4] = mul_p(u[4], w4, p4);
-            u[5] = mul(u[5], mul_p(w1, w4, p4));
-            u[6] = mul(u[6], mul_p(w2, w4, p4));
-            u[7] = mul(u[7], mul_p(w3, w4, p4));
+            const c2 w4 = mul(w2, w2);
+            u[4] = mul_tw<DIR>(u[4], w4);
+            u[5] = mul_tw<DIR>(u[5], mul(w1, w4));
+            u[6] = mul_tw<DIR>(u[6], mul(w2, w4));
+            u[7] = mul_tw<DIR>(u[7], mul(w3, w4));
             if constexpr (R >= 16) {
-                const c2 w8 = mul_p(w4, w4, p4), p8 = prime(w8);
-                u[8] = mul_p(u[8], w8, p8);
-                u[9] = mul(u[9], mul_p(w1, w8, p8));
-                u[10] = mul(u[10], mul_p(w2, w8, p8));
-                u[11] = mul(u[11], mul_p(w3, w8, p8));
-                const c2 w12 = mul_p(w4, w8, p8), p12 = prime(w12);
-                u[12] = mul_p(u[12], w12, p12);
-                u[13] = mul(u[13], mul_p(w1, w12, p12));
-                u[14] = mul(u[14], mul_p(w2, w12, p12));
-                u[15] = mul(u[15], mul_p(w3, w12, p12));
+                const c2 w8 = mul(w4, w4);
+                u[8] = mul_tw<DIR>(u[8], w8);
+                u[9] = mul_tw<DIR>(u[9], mul(w1, w8));
+                u[10] = mul_tw<DIR>(u[10], mul(w2, w8));
+                u[11] = mul_tw<DIR>(u[11], mul(w3, w8));
+                const c2 w12 = mul(w4, w8);
+                u[12] = mul_tw<DIR>(u[12], w12);
+                u[13] = mul_tw<DIR>(u[13], mul(w1, w12));
+                u[14] = mul_tw<DIR>(u[14], mul(w2, w12));
+                u[15] = mul_tw<DIR>(u[15], mul(w3, w12));
             }
         }
     }
 }
 
-// Twiddle W_N^idx from the device table tw[idx] = exp(-2*pi*i*idx/N).
-template <int DIR>
-__device__ __forceinline__ c2 twiddle(const c2 *__restrict__ tw, int idx)
-{
-    c2 w = tw[idx];
-    return DIR < 0 ? w : mk(w.x, -w.y);
-}
 
 constexpr int fft_passes_v(int log2n) { return log2n / 3 + (log2n % 3 ? 1 : 0); }
 template <int LOG2N> constexpr int fft_passes() { return fft_passes_v(LOG2N); }
@@ -157,17 +178,19 @@ constexpr int pass_ns_v(int log2n, int p) { return p == 0 ? 1 : pass_ns_v(log2n,
 // path; powers are products of one preloaded base instead.
 constexpr int tw_entries_v(int log2n) { return 1 << log2n; }
 
-// Base twiddle W_{Ns R}^r of butterfly q of pass P (one table load), for every
-// pass, issued at FFT start so the latency hides under pass 0: slot P*4 + q.
-template <int LOG2N, int DIR, int P = 1>
+// Base twiddle W_{Ns R}^r of butterfly q of pass P (one load from the table
+// tw[k] = exp(-2 pi i k / N)), for every pass, issued at FFT start so the
+// latency hides under pass 0: slot P*4 + q.  Always the forward base: the
+// inverse conjugates in its multiplies (mul_tw).
+template <int LOG2N, int P = 1>
 __device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
 {
     if constexpr (P < fft_passes<LOG2N>()) {
         constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
         constexpr int NS = pass_ns_v(LOG2N, P), TWS = N / (NS * R);
 #pragma unroll
-        for (int q = 0; q < B; ++q) wb[P * 4 + q] = twiddle<DIR>(tw, ((t + q * T) & (NS - 1)) * TWS);
-        preload_twiddles<LOG2N, DIR, P + 1>(wb, t, tw);
+        for (int q = 0; q < B; ++q) wb[P * 4 + q] = tw[((t + q * T) & (NS - 1)) * TWS];
+        preload_twiddles<LOG2N, P + 1>(wb, t, tw);
     }
 }
 
@@ -201,7 +224,7 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
         c2 u[R];
 #pragma unroll
         for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
-        if constexpr (NS > 1) apply_twiddles<R>(u, wb[P * 4 + q]);
+        if constexpr (NS > 1) apply_twiddles<R, DIR>(u, wb[P * 4 + q]);
         if constexpr (R == 8) dft8<DIR>(u);
         else if constexpr (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
         else dft2<DIR>(u[0], u[1]);
@@ -245,7 +268,7 @@ template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
 {
     c2 wb[16];
-    preload_twiddles<LOG2N, DIR>(wb, t, tw);
+    preload_twiddles<LOG2N>(wb, t, tw);
     fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wb);
 }
 
@@ -255,20 +278,12 @@ constexpr bool tw_slot_used(int log2n, int i)
     return i / 4 >= 1 && i / 4 < fft_passes_v(log2n) && i % 4 < 8 / pass_radix_v(log2n, i / 4);
 }
 
-// Same, with the forward-direction twiddle bases already in registers
-// (preload_twiddles<LOG2N, -1>; the inverse uses their conjugates): for loops
-// that must not issue loads between frames.
+// Same, with the (forward) twiddle bases already in registers
+// (preload_twiddles): for loops that must not issue loads between frames.
 template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs_w(c2 (&v)[8], int t, c2 *lds, const c2 (&wf)[16])
 {
-    if constexpr (DIR < 0) {
-        fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wf);
-    } else {
-        c2 wb[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) wb[i] = mk(wf[i].x, -wf[i].y);
-        fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wb);
-    }
+    fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wf);
 }
 
 }  // namespace mm

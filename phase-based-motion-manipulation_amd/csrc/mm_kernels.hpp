@@ -415,7 +415,7 @@ __device__ __forceinline__ c2 pyramid_op(c2 c, c2 p, int fx, int fy, const Spec 
         const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
         const float ph = sp.S * d;
         const float k = mmag * sp.inv_nn;
-        a = add(a, scale(mul(c, mk(__cosf(ph), __sinf(ph))), k));
+        a = add(a, scale(mul_c(c, mk(__cosf(ph), __sinf(ph))), k));
     }
     return a;
 }
@@ -444,7 +444,7 @@ __device__ __forceinline__ c2 standard_op(c2 c, c2 p, int fx, int fy, const Spec
     }
     const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
     const float ph = (d * w) * sp.S;
-    return scale(mul(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
+    return scale(mul_c(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
 }
 
 template <int LOG2N, int MODE>
@@ -559,7 +559,24 @@ __device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spe
         const float rev = atan2_nz(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y) * sp.S_rev;
         w = mk(mmag * __builtin_amdgcn_cosf(rev) + mpass, mmag * __builtin_amdgcn_sinf(rev));
     }
-    return mul(c, w);
+    return mul_c(c, w);
+}
+
+// pyramid_op_t for a bin with at most one middle band (table entry y < 0,
+// the usual case: bands touch only where their masks are 0), without
+// branches: the gated-in phase factor is computed for every bin and selected
+// at the end, so the compiler can interleave several bins' dependency chains
+// (atan2 polynomial, v_sin/v_cos) instead of running them one after another.
+__device__ __forceinline__ c2 pyramid_op_1band(c2 c, c2 p, const Spec &sp, float2 mt)
+{
+    const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
+    const bool gate = mt.x * mt.x * mn2 < sp.tau2_nn;
+    const float mpass = gate ? mt.x - mt.y : -mt.y;
+    const float mmag = gate ? 0.0f : mt.x;
+    const float rev = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y) * sp.S_rev;
+    const float cw = __builtin_amdgcn_cosf(rev), sw = __builtin_amdgcn_sinf(rev);
+    const c2 w = mmag > 0.0f ? mk(mmag * cw + mpass, mmag * sw) : mk(mpass, 0.0f);
+    return mul_c(c, w);
 }
 
 template <int MODE>
@@ -569,7 +586,7 @@ __device__ __forceinline__ c2 standard_op_t(c2 c, c2 p, const Spec &sp, float2 m
     if (mn2 < sp.tau2) return scale(c, sp.inv_nn);
     const float d = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y);
     const float ph = (d * mt.x) * sp.S;
-    return scale(mul(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
+    return scale(mul_c(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
 }
 
 // MODE: MM_MODE_PYRAMID (dynamic masks), MM_MODE_STANDARD or MM_K2_PYR_TAB (tables)
@@ -612,11 +629,32 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 // grid is then exactly N/2 groups (512 two-column workgroups at N=2048: one
 // resident round at 2 WGs/CU, no one-group tail).  Column N/2's F_{t-1} stays
 // in LDS (ldsN) across the frames of a launch.
-template <int LOG2N, int MODE>
-__global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
-void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
-            const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
-            Geo g, Spec sp, const c2 *__restrict__ tw)
+#ifndef MM_K2_OPG
+#define MM_K2_OPG 8   // bins of the branch-free op interleaved per scheduling group
+#endif
+#ifdef MM_K2_STAMPS
+// Diagnostic build only: per-wave cycle totals of the frame-loop phases
+// (s_memtime deltas), written by lane 0 with a vector store after the loop.
+__device__ unsigned long long mm_k2_stamps[4096 * 8 * 8];
+#define K2_STAMP(i)                                                      \
+    do {                                                                 \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();      \
+        st_acc[i] += n_ - st_prev;                                       \
+        st_prev = n_;                                                    \
+    } while (0)
+#else
+#define K2_STAMP(i) do { } while (0)
+#endif
+//
+// The frame loop is instantiated twice (BLK0): block 0, whose group 0 is the
+// packed group, runs the extra exchanges; every other block runs a loop with
+// none of that code, so its register allocation is not shaped by the packed
+// group's live values.
+template <int LOG2N, int MODE, bool BLK0>
+__device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,
+                                            const c2 *state_in, c2 *state_out, int nframes,
+                                            int first_passthrough, const Geo &g, const Spec &sp,
+                                            const c2 *__restrict__ tw, int blk)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     constexpr int TE = k2_tab_entries<LOG2N>();
@@ -632,13 +670,10 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
     // store the next frame's loads must wait for)
     c2 *ldsN = reinterpret_cast<c2 *>(tabN + TE);
     float *stgN = reinterpret_cast<float *>(ldsN + N / 2 + 1);
-    // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
-    // are merged in one L2 (split over XCDs they left as partial-line writes)
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
-    const bool blk0 = blk == 0;               // uniform: block 0 runs the extra exchanges
+    constexpr bool blk0 = BLK0;               // block 0 runs the extra exchanges
     const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
     c2 *stN = state_out + (size_t)(N / 2) * N;
 
@@ -656,6 +691,18 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
         __syncthreads();
     }
 
+    // waves whose bins all have at most one middle band (frame-invariant,
+    // uniform) take the branch-free op
+    bool wave_two_band = true;
+    if constexpr (MODE == MM_K2_PYR_TAB) {
+        bool two = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int fy = t0 + j * T;
+            two |= !__builtin_signbit(tab0[fy <= N / 2 ? fy : N - fy].y);
+        }
+        wave_two_band = __any(two);
+    }
     c2 prev[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -669,9 +716,13 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
         }
     }
 
-    // G column of a frame: unconditional loads at clamped rows, selected at use.
-    // A frame's loads are issued before the previous frame's Q stores, so the
-    // wait for them does not wait for those stores (one in-order vmcnt).
+    // G column of a frame.  Rows outside the image get an out-of-range buffer
+    // offset: the range check returns 0 for them without a memory access (the
+    // zero padding of PadTexture, .cs:358-381).  A frame's loads are issued
+    // before the previous frame's Q stores, so the wait for them never waits
+    // for those stores (one in-order vmcnt).  (Loading one frame ahead, 16
+    // more VGPRs, measured no faster: the frame loop is bound by its barrier
+    // and dependency-chain latencies, not by this load's.)
     c2 ga[8];
     float gb[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     // (buffer loads: 32-bit offsets, and kept in order with the buffer stores)
@@ -681,17 +732,18 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                                                            (int)(g_stride * sizeof(c2)), 0x00020000);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int rc = min(max(t + j * T - g.y0, 0), g.H - 1);
+            const int rr = t + j * T - g.y0;
+            const unsigned off = rr >= 0 && rr < g.H ? (unsigned)(f * g.H + rr) * 8u : 0x80000000u;
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, (unsigned)(f * g.H + rc) * 8u, 0, 0);
+            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, off, 0, 0);
             ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
         }
-        if (blk0) {   // column N/2 (real) for the packed group's block only
+        if constexpr (blk0) {   // column N/2 (real) for the packed group's block only
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int rc = min(max(t + j * T - g.y0, 0), g.H - 1);
-                gb[j] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(grs, (unsigned)((N / 2) * g.H + rc) * 8u, 0, 0));
+                const int rr = t + j * T - g.y0;
+                const unsigned off = rr >= 0 && rr < g.H ? (unsigned)((N / 2) * g.H + rr) * 8u : 0x80000000u;
+                gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, off, 0, 0));
             }
         }
     };
@@ -699,7 +751,7 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles<LOG2N, -1>(wtw, t0, tw);
+    preload_twiddles<LOG2N>(wtw, t0, tw);
     constexpr int TK = q_tile<LOG2N>(), BLK = GPW * TK / 2;   // float4 per tile row
     constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
     const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
@@ -711,6 +763,10 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
     // thread; slots past the end are dropped by the range check), then frame
     // fr, whose first use of the loads waits with vmcnt(NST) and never for the
     // stores.
+#ifdef MM_K2_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#endif
     for (int fr = 0;; ++fr) {
         // Opaque per-iteration copy of the lane index: stops LICM from hoisting
         // every t-derived LDS address and twiddle of both FFTs out of the frame
@@ -718,6 +774,7 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
         int t = t0;
         asm volatile("" : "+v"(t));
         load_g(fr < nframes ? fr : nframes - 1, t);
+        K2_STAMP(0);
         __builtin_amdgcn_sched_barrier(0);   // keep the stores behind the loads
         {
             float4 sv[NST];
@@ -742,14 +799,13 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                                  __float_as_uint(sv[i].z), __float_as_uint(sv[i].w)};
                 __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so[i], 0, 0);
             }
-            // column N/2 of frame fr-1 (block 0 only; elsewhere dropped stores
-            // keep the count static).  Read after the barrier: stgN is rewritten
-            // only after the packed section's first barrier below.
-            constexpr int NSTN = (N / 2 + GPW * T - 1) / (GPW * T);
+            // column N/2 of frame fr-1 (block 0 only).  Read after the barrier:
+            // stgN is rewritten only after the packed section's first barrier below.
+            constexpr int NSTN = blk0 ? (N / 2 + GPW * T - 1) / (GPW * T) : 0;
 #pragma unroll
             for (int i = 0; i < NSTN; ++i) {
                 const int e = grp * T + t + i * GPW * T;
-                const bool ok = staged && blk0 && e < g.Hq / 2;   // rows 2e, 2e+1 (one tile: TK even)
+                const bool ok = staged && e < g.Hq / 2;   // rows 2e, 2e+1 (one tile: TK even)
                 const float2 p = reinterpret_cast<const float2 *>(stgN)[ok ? e : 0];
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                 const u32x4 d = {__float_as_uint(p.x), 0u, __float_as_uint(p.y), 0u};
@@ -757,28 +813,27 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                     d, qrs, ok ? (unsigned)(((2 * e) / TK * g.Qs + N / 2) * TK + (2 * e) % TK) * 8u : 0x80000000u, 0, 0);
             }
         }
+        K2_STAMP(1);
         if (fr == nframes) break;
+        c2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)   // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
+            v[j] = packed ? mk(ga[j].x, gb[j]) : ga[j];
         // opaque per-iteration copy of the twiddle bases (same reason as t: the
         // products of their powers must not be hoisted into live registers)
         c2 wt[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             wt[i] = wtw[i];
-            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
         }
-        c2 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int rr = t + j * T - g.y0;
-            const bool in = rr >= 0 && rr < g.H;
-            // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
-            v[j] = in ? (packed ? mk(ga[j].x, gb[j]) : ga[j]) : mk(0.0f, 0.0f);
-        }
+        K2_STAMP(2);
         MM_MARK("M1_fwd_start");
         fft_regs_w<LOG2N, -1>(v, t, lds, wt);
         MM_MARK("M2_fwd_end");
+        K2_STAMP(3);
         const bool pass_frame = fr == 0 && first_passthrough;
-        if (blk0) {
+        if constexpr (blk0) {
             // packed group: Z = F0 + i FN.  Upper half of Z to LDS for the partner
             // reads (bins fy <= N/2 live in j < 4, plus fy = N/2 at t = 0, j = 4).
             if (packed) {
@@ -828,7 +883,19 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
                 for (int j = 0; j < 8; ++j) prev[j] = v[j];
             }
         } else {
-        if (!packed) {
+        if (!packed && MODE == MM_K2_PYR_TAB && !wave_two_band) {
+            // no bin of this wave has two middle bands: branch-free op, bins
+            // interleaved MM_K2_OPG at a time
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
+                const int fy = t + j * T;
+                const c2 a = pyramid_op_1band(v[j], prev[j], sp, tab0[fy <= N / 2 ? fy : N - fy]);
+                prev[j] = v[j];
+                v[j] = a;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        } else if (!packed) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 // one bin at a time: keeps the 8 op instances from being interleaved
@@ -839,9 +906,11 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        K2_STAMP(4);
         MM_MARK("M3_inv_start");
         fft_regs_w<LOG2N, +1>(v, t, lds, wt);
         MM_MARK("M4_inv_end");
+        K2_STAMP(5);
         // Q is stored by row pairs (q_index) so that K3 reads each of its two
         // rows' values as one 16-B piece per bin, contiguous across the wave (a
         // column-major Q made K3's 16-B gathers cost it 4 of its 7 us/frame at
@@ -864,7 +933,14 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
         }
         }   // !pass_frame
         __syncthreads();   // staged pieces complete (stored at the top of the next iteration)
+        K2_STAMP(6);
     }
+#ifdef MM_K2_STAMPS
+    if (threadIdx.x % 64 == 0) {
+        const int w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
+    }
+#endif
     if (valid) {
         if (packed) {
             // column 0: bins fy <= N/2 in prev[0..4]; the rest is the Hermitian
@@ -889,6 +965,27 @@ void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restr
             for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t0 + j * T] = prev[j];
         }
     }
+}
+
+#ifndef MM_K2_WAVES
+#define MM_K2_WAVES 4
+#endif
+
+template <int LOG2N, int MODE>
+__global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
+void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
+            const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
+            Geo g, Spec sp, const c2 *__restrict__ tw)
+{
+    // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
+    // are merged in one L2 (split over XCDs they left as partial-line writes)
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    if (blk == 0)
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Q, q_stride, state_in, state_out, nframes,
+                                       first_passthrough, g, sp, tw, blk);
+    else
+        k_cols_body<LOG2N, MODE, false>(G, g_stride, Q, q_stride, state_in, state_out, nframes,
+                                        first_passthrough, g, sp, tw, blk);
 }
 
 // =========================================================================

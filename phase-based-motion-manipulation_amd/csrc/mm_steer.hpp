@@ -144,7 +144,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles<LOG2N, -1>(wtw, t0, tw);
+    preload_twiddles<LOG2N>(wtw, t0, tw);
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
     const int kx0 = blk * GPW;
@@ -158,7 +158,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             wt[i] = wtw[i];
-            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
         }
         const int o = nmid ? b / nmid : 0, i = nmid ? 1 + b % nmid : 0;
         // workgroup-uniform: skip the band where all its columns are zero
@@ -236,7 +236,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles<LOG2N, -1>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
+    preload_twiddles<LOG2N>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
     // row k of band b (contiguous) and its state: loaded one band ahead
     c2 v[8];
     float pp[8], puh[8], pul[8];
@@ -276,7 +276,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             wt[i] = wtw[i];
-            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i].x), "+v"(wt[i].y));
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
         }
         fft_regs_w<LOG2N, +1>(v, t, lds, wt);
         if (b == nb) {   // residual: Hermitian, real output
@@ -306,7 +306,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
             c2 s2 = v[j];
             if (write_out && v[j].x * v[j].x + v[j].y * v[j].y >= sp.tau2) {
                 const float rev = P * sp.S_rev;
-                s2 = mul(v[j], mk(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)));
+                s2 = mul_c(v[j], mk(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)));
             }
             const int xi = (t + j * T - xs + N) & (N - 1);
             if (xi < Wc) y[j] += 2.0f * s2.x;

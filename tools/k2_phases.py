@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""k_cols phase breakdown from a diagnostic build (-DMM_K2_STAMPS): cycles per
+frame of each frame-loop phase, averaged over waves (s_memtime deltas taken by
+every wave; block 0 reported separately).
+
+usage: MM355_LIB=lib/variants/stamps.so python3 tools/k2_phases.py [frames]
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "phase-based-motion-manipulation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import mm355  # noqa: E402
+
+PHASES = ["top+loads", "stores+barrier", "G wait+setup", "fwd FFT", "op", "inv FFT", "stage+barrier"]
+W, H = 1920, 1080
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
+h.set_batch(n)
+fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+out = torch.empty_like(fr)
+h.synth(fr, 0, n)
+h.process_stream(fr, out, n, mm355.RGBA8)      # warm-up (first frame passthrough)
+torch.cuda.synchronize()
+h.process_stream(fr, out, n, mm355.RGBA8)      # the launch whose stamps are read
+torch.cuda.synchronize()
+L = mm355.lib()
+nw = 4096
+buf = (ctypes.c_ulonglong * (nw * 8))()
+L.mm_debug_k2_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+assert L.mm_debug_k2_stamps(buf, nw * 8) == 0
+a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8)[:, :len(PHASES)].astype(np.float64) / n
+waves = (h.N // 2 + 1) // 2 * 8 if False else nw
+live = a[a.sum(axis=1) > 0]
+res = {"frames": n, "waves": int(live.shape[0]),
+       "cycles_per_frame_mean": {p: round(float(live[:, i].mean()), 1) for i, p in enumerate(PHASES)},
+       "cycles_per_frame_block0": {p: round(float(a[:8, i].mean()), 1) for i, p in enumerate(PHASES)},
+       "total_mean": round(float(live.sum(axis=1).mean()), 1),
+       "total_max": round(float(live.sum(axis=1).max()), 1)}
+print(json.dumps(res))

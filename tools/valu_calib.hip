@@ -42,8 +42,20 @@ __global__ void valu(float *out, Stamp *st, float a, float b)
                 x[c] = x[c] + a;
             } else if constexpr (KIND == 2) {   // v_sin_f32 (transcendental)
                 x[c] = __builtin_amdgcn_sinf(x[c]);
-            } else {                            // v_pk_fma_f32 (two floats per lane)
+            } else if constexpr (KIND == 3) {   // v_pk_fma_f32 (two floats per lane)
                 xp[c] = __builtin_elementwise_fma(xp[c], ap, bp);
+            } else if constexpr (KIND == 4) {   // v_pk_add_f32
+                asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(xp[c]) : "v"(bp));
+            } else if constexpr (KIND == 5) {   // v_pk_mul_f32
+                asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(xp[c]) : "v"(ap));
+            } else if constexpr (KIND == 6) {   // v_pk_fma_f32 with op_sel/neg swizzles (complex multiply half)
+                asm volatile("v_pk_fma_f32 %0, %0, %1, %2 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+                             : "+v"(xp[c]) : "v"(ap), "v"(bp));
+            } else if constexpr (KIND == 7) {   // v_pk_add_f32 with op_sel swizzle (+-i rotation)
+                asm volatile("v_pk_add_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+                             : "+v"(xp[c]) : "v"(bp));
+            } else {                            // v_mul_f32 + v_add_f32 pair (scalar reference for 6/7)
+                x[c] = x[c] * a + b;
             }
         }
         asm volatile("" ::: "memory");
@@ -97,15 +109,18 @@ static double run(int waves_per_simd, double *clk_ghz, float *ms_out)
 
 int main()
 {
-    const char *names[4] = {"v_fma_f32", "v_add_f32", "v_sin_f32", "v_pk_fma_f32"};
+    const char *names[8] = {"v_fma_f32", "v_add_f32", "v_sin_f32", "v_pk_fma_f32", "v_pk_add_f32",
+                            "v_pk_mul_f32", "v_pk_fma_f32 op_sel", "v_pk_add_f32 op_sel"};
     printf("{\"iters\": %d, \"chains\": %d, \"rows\": [\n", ITERS, CHAINS);
     bool first = true;
-    for (int kind = 0; kind < 4; ++kind)
+    for (int kind = 0; kind < 8; ++kind)
         for (int w : {1, 2, 4, 8}) {
             double clk = 0;
             float ms = 0;
             double cyc = kind == 0 ? run<0>(w, &clk, &ms) : kind == 1 ? run<1>(w, &clk, &ms)
-                       : kind == 2 ? run<2>(w, &clk, &ms) : run<3>(w, &clk, &ms);
+                       : kind == 2 ? run<2>(w, &clk, &ms) : kind == 3 ? run<3>(w, &clk, &ms)
+                       : kind == 4 ? run<4>(w, &clk, &ms) : kind == 5 ? run<5>(w, &clk, &ms)
+                       : kind == 6 ? run<6>(w, &clk, &ms) : run<7>(w, &clk, &ms);
             printf("%s {\"inst\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"clock_GHz\": %.3f, "
                    "\"cycles_per_wave_inst\": %.3f}",
                    first ? "" : ",\n", names[kind], w, ms, clk, cyc);
