@@ -1,0 +1,70 @@
+/*
+ * mm_ring.h — frame-sharded streaming over an RCCL ring, in C.
+ *
+ * One process per GPU.  Output frame t of the reference operator depends only
+ * on input frames t-1 and t (MotionMagnificationProcessor.cs:142 keeps the
+ * previous input as the only state), and that state is a pure function of
+ * input t-1 (mm_compute_state).  So a stream shards into contiguous per-rank
+ * chunks and the only exchange is ONE ring shift per step:
+ *
+ *   step s, world G, chunk C: rank g owns frames [s*G*C + g*C, s*G*C + (g+1)*C)
+ *   1. st_out = state of my last frame of step s (from my own input)
+ *   2. ncclSend(st_out -> g+1), ncclRecv(st_in <- g-1)   (one group call)
+ *   3. rank g > 0: state := st_in of step s;  rank 0: state := st_in of step
+ *      s-1 (rank G-1's last frame of the previous step); at s = 0: reset
+ *      (the stream's first frame passes through, .cs:111-117)
+ *   4. mm_process_stream over my C frames
+ *
+ * Steps 1-2 of step s+1 are posted before step s's frames are processed (the
+ * shift runs on the ring's own HIP stream under step s's kernels; one chunk
+ * of input lookahead), as mm355.stream.ShardedStream(prefetch=True) does in
+ * Python.  The state buffers are device memory (mm_state_size bytes).
+ *
+ * This module links RCCL (librccl); the frame operator itself (libmm355) does
+ * not.  Return codes are the MM_* codes of mm.h; an RCCL failure is MM_ERR_HIP
+ * (mm_ring_last_error() gives RCCL's message).
+ */
+#ifndef MM_RING_H
+#define MM_RING_H
+
+#include <stddef.h>
+
+#include "mm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MM_RING_ID_BYTES 128   /* == NCCL_UNIQUE_ID_BYTES */
+
+typedef struct mm_ring mm_ring;
+
+/* Rank 0 generates the ring id and hands it to every rank out of band (a
+ * file, a launcher, MPI ...).  Replaces torch.distributed's rendezvous. */
+int mm_ring_get_id(unsigned char id[MM_RING_ID_BYTES]);
+
+/* Joins the ring as `rank` of `world` on HIP device `hip_device`, for the
+ * width x height stream processed by handle `h` (same device, same geometry)
+ * in chunks of `chunk` frames of `format` (MM_RGBA8 / MM_RGBA32F).  world may
+ * be 1 (the shift is then a send to and a receive from itself). */
+int mm_ring_create(int world, int rank, const unsigned char id[MM_RING_ID_BYTES], int hip_device,
+                   mm_handle *h, int width, int height, int chunk, int format, mm_ring **out);
+
+/* Runs step `step` (steps in order from 0): `in` = this rank's C input frames
+ * of the step, `out` = their C output frames, `next_last` = the LAST input
+ * frame of this rank's chunk of step+1 (posts that step's shift ahead), or
+ * NULL for the final step.  All device pointers; work is ordered on
+ * `hip_stream` (NULL: the default stream).  Asynchronous like mm_process_stream. */
+int mm_ring_step(mm_ring *r, int step, const void *in, void *out, const void *next_last,
+                 void *hip_stream);
+
+/* Waits for every posted shift (a shift posted for a step that is never run
+ * included) and releases the ring. */
+void mm_ring_destroy(mm_ring *r);
+
+const char *mm_ring_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MM_RING_H */

@@ -182,15 +182,17 @@ constexpr int tw_entries_v(int log2n) { return 1 << log2n; }
 // tw[k] = exp(-2 pi i k / N)), for every pass, issued at FFT start so the
 // latency hides under pass 0: slot P*4 + q.  Always the forward base: the
 // inverse conjugates in its multiplies (mul_tw).
-template <int LOG2N, int P = 1>
+// TWST: stride of the table actually passed (a W_{N*TWST} table serves a
+// length-N transform at indices times TWST).
+template <int LOG2N, int P = 1, int TWST = 1>
 __device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
 {
     if constexpr (P < fft_passes<LOG2N>()) {
         constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
         constexpr int NS = pass_ns_v(LOG2N, P), TWS = N / (NS * R);
 #pragma unroll
-        for (int q = 0; q < B; ++q) wb[P * 4 + q] = tw[((t + q * T) & (NS - 1)) * TWS];
-        preload_twiddles<LOG2N, P + 1>(wb, t, tw);
+        for (int q = 0; q < B; ++q) wb[P * 4 + q] = tw[((t + q * T) & (NS - 1)) * TWS * TWST];
+        preload_twiddles<LOG2N, P + 1, TWST>(wb, t, tw);
     }
 }
 
@@ -212,7 +214,18 @@ __host__ __device__ constexpr int xpad(int i) { return i + xpad_a(LOG2N, NS) * (
 // One Stockham pass (radix R, stride Ns).  B = 8/R butterflies per thread;
 // butterfly b = t + q*T reads x[b + m*N/R] (= register q + m*B) and writes
 // y[(b/Ns)*Ns*R + b%Ns + m*Ns].
-template <int LOG2N, int P, int DIR>
+// Exchange synchronisation: WSYNC = false -> workgroup barriers (the group
+// spans several waves); true -> the group lies within one wave, whose LDS
+// operations execute in program order, so only the compiler's ordering of
+// the writes before the reads is needed (wave_barrier: no s_barrier).
+template <bool WSYNC>
+__device__ __forceinline__ void xsync()
+{
+    if constexpr (WSYNC) __builtin_amdgcn_wave_barrier();
+    else __syncthreads();
+}
+
+template <int LOG2N, int P, int DIR, bool WSYNC = false>
 __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
 {
     constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
@@ -239,7 +252,7 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
         }
     }
     if constexpr (!LAST) {
-        __syncthreads();
+        xsync<WSYNC>();
         if constexpr (T % 32 == 0) {   // xpad(t + j T) = xpad(t) + xpad(j T)
             const c2 *col = lds + xpad<LOG2N, NS>(t);
 #pragma unroll
@@ -248,16 +261,16 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = lds[xpad<LOG2N, NS>(t + j * T)];
         }
-        __syncthreads();
+        xsync<WSYNC>();
     }
 }
 
-template <int LOG2N, int DIR, int P>
+template <int LOG2N, int DIR, int P, bool WSYNC = false>
 __device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
 {
     if constexpr (P < fft_passes<LOG2N>()) {
-        fft_pass<LOG2N, P, DIR>(v, t, lds, wb);
-        fft_pass_loop<LOG2N, DIR, P + 1>(v, t, lds, wb);
+        fft_pass<LOG2N, P, DIR, WSYNC>(v, t, lds, wb);
+        fft_pass_loop<LOG2N, DIR, P + 1, WSYNC>(v, t, lds, wb);
     }
 }
 
@@ -284,6 +297,124 @@ template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs_w(c2 (&v)[8], int t, c2 *lds, const c2 (&wf)[16])
 {
     fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wf);
+}
+
+// ---- wave-local FFT: one barrier per transform ------------------------------
+// For N >= 1024 a group of T = N/8 threads spans C = N/512 waves.  N = C x M,
+// M = 512 = 64 lanes x 8 points: an outer C-point stage across the waves (in
+// registers: thread t holds, for each of its H = 8/C values n2 = t + 64 C h,
+// all C elements n2 + M n1 in registers h + H n1), ONE cross-wave exchange
+// through LDS, and an inner M-point Stockham FFT per wave whose two exchanges
+// are wave-local (no s_barrier).  Against the all-workgroup Stockham form (six
+// barriers per transform at N = 2048) this removes five barrier waits and
+// their skew; the LDS bytes moved are the same.
+//   fft_dif: natural order in (v[j] = x[t + jT]), bin-permuted out:
+//            v[j] = X[w + C (l + 64 j)], w = t / 64, l = t % 64 (fft_bin).
+//   fft_dit: bin-permuted in, natural order out (the inverse of that layout).
+// For N <= 512 (C = 1) both are the plain Stockham transform, synchronised per
+// wave (a group lies within one wave).
+// LDS: C regions of fft_region() complex values (= lds_complex<N>() in all);
+// region w is wave w's for the inner transform.  On return from either, other
+// waves may still use their regions: __syncthreads() before any use of the
+// group's LDS by another wave.
+constexpr int fft_c_v(int log2n) { return log2n >= 9 ? 1 << (log2n - 9) : 1; }
+constexpr int fft_inner_v(int log2n) { return log2n >= 9 ? 9 : log2n; }
+constexpr int fft_region_v(int log2n) { return (1 << fft_inner_v(log2n)) + (1 << fft_inner_v(log2n)) / 8; }
+
+// Slot i of the fft_dif / fft_dit twiddle-base array is in use.
+constexpr bool tw_slot_used_wl(int log2n, int i)
+{
+    return fft_c_v(log2n) == 1 ? tw_slot_used(log2n, i)
+                               : (i == 4 || i == 8 || (i >= 12 && i < 12 + 8 / fft_c_v(log2n)));
+}
+
+// bin of register j of thread t after fft_dif (and before fft_dit)
+template <int LOG2N>
+__device__ __forceinline__ int fft_bin(int t, int j)
+{
+    constexpr int C = fft_c_v(LOG2N), T = (1 << LOG2N) / 8;
+    if constexpr (C == 1) return t + j * T;
+    else return (t >> 6) + C * ((t & 63) + 64 * j);
+}
+
+// Twiddle bases of fft_dif / fft_dit (forward direction): the inner passes'
+// (slots 4, 8, from the W_N table at stride C) and, for C > 1, the outer
+// stage's W_N^{n2} for the thread's H values n2 (slots 12 + h).
+template <int LOG2N>
+__device__ __forceinline__ void preload_twiddles_wl(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
+{
+    constexpr int C = fft_c_v(LOG2N);
+    if constexpr (C == 1) {
+        preload_twiddles<LOG2N>(wb, t, tw);
+    } else {
+        preload_twiddles<9, 1, C>(wb, t & 63, tw);
+#pragma unroll
+        for (int h = 0; h < 8 / C; ++h) wb[12 + h] = tw[t + 64 * C * h];
+    }
+}
+
+template <int C, int DIR>
+__device__ __forceinline__ void dft_c(c2 *u)
+{
+    if constexpr (C == 8) dft8<DIR>(u);
+    else if constexpr (C == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
+    else dft2<DIR>(u[0], u[1]);
+}
+
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+{
+    constexpr int C = fft_c_v(LOG2N), H = 8 / C, RS = fft_region_v(LOG2N);
+    if constexpr (C == 1) {
+        fft_pass_loop<LOG2N, DIR, 0, true>(v, t, lds, wb);
+    } else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            c2 u[C];
+#pragma unroll
+            for (int m = 0; m < C; ++m) u[m] = v[h + H * m];
+            dft_c<C, DIR>(u);                       // over n1 -> k1
+            apply_twiddles<C, DIR>(u, wb[12 + h]);  // Y[k1] *= W_N^{n2 k1}
+            const int n2 = t + 64 * C * h;
+#pragma unroll
+            for (int m = 0; m < C; ++m) lds[m * RS + n2] = u[m];
+        }
+        __syncthreads();
+        const int w = t >> 6, l = t & 63;
+        c2 *reg = lds + w * RS;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = reg[l + 64 * j];
+        __builtin_amdgcn_wave_barrier();
+        fft_pass_loop<9, DIR, 0, true>(v, l, reg, wb);
+    }
+}
+
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void fft_dit(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+{
+    constexpr int C = fft_c_v(LOG2N), H = 8 / C, RS = fft_region_v(LOG2N);
+    if constexpr (C == 1) {
+        fft_pass_loop<LOG2N, DIR, 0, true>(v, t, lds, wb);
+    } else {
+        const int w = t >> 6, l = t & 63;
+        c2 *reg = lds + w * RS;
+        fft_pass_loop<9, DIR, 0, true>(v, l, reg, wb);   // over k2 -> n2, region w
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) reg[l + 64 * j] = v[j];
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            const int n2 = t + 64 * C * h;
+            c2 u[C];
+#pragma unroll
+            for (int m = 0; m < C; ++m) u[m] = lds[m * RS + n2];
+            apply_twiddles<C, DIR>(u, wb[12 + h]);  // y[k1] *= W_N^{DIR n2 k1}
+            dft_c<C, DIR>(u);                       // over k1 -> n1
+#pragma unroll
+            for (int m = 0; m < C; ++m) v[h + H * m] = u[m];
+        }
+    }
 }
 
 }  // namespace mm

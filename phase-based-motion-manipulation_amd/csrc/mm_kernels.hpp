@@ -304,10 +304,13 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         const bool in = valid && i >= 0 && i < g.W;
         v[j] = in ? mk(ya, yb) : mk(0.0f, 0.0f);
     }
+    c2 wb[16];
+    preload_twiddles_wl<LOG2N>(wb, t, tw);
     __syncthreads();
-    fft_regs<LOG2N, -1>(v, t, lds, tw);
+    fft_dif<LOG2N, -1>(v, t, lds, wb);
+    __syncthreads();   // every wave done with its LDS region
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lds[pad8(t + j * T)] = v[j];
+    for (int j = 0; j < 8; ++j) lds[pad8(fft_bin<LOG2N>(t, j))] = v[j];
     __syncthreads();
     // half spectra of rows (ra, ra+1) at bins f = t + jT (j < 4) and N/2 (j = 4)
     auto split = [&](int f) {
@@ -698,7 +701,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         bool two = false;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int fy = t0 + j * T;
+            const int fy = fft_bin<LOG2N>(t0, j);
             two |= !__builtin_signbit(tab0[fy <= N / 2 ? fy : N - fy].y);
         }
         wave_two_band = __any(two);
@@ -706,11 +709,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     c2 prev[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-        prev[j] = state_in ? state_in[(size_t)f * N + t0 + j * T] : mk(0.0f, 0.0f);
+        prev[j] = state_in ? state_in[(size_t)f * N + fft_bin<LOG2N>(t0, j)] : mk(0.0f, 0.0f);
     if (packed) {   // each thread reads and writes only its own bins: no barrier
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-            const int fy = t0 + j * T;
+            const int fy = fft_bin<LOG2N>(t0, j);
             if (j < 4 || fy == N / 2)
                 ldsN[fy] = state_in ? state_in[(size_t)(N / 2) * N + fy] : mk(0.0f, 0.0f);
         }
@@ -751,7 +754,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles<LOG2N>(wtw, t0, tw);
+    preload_twiddles_wl<LOG2N>(wtw, t0, tw);
     constexpr int TK = q_tile<LOG2N>(), BLK = GPW * TK / 2;   // float4 per tile row
     constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
     const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
@@ -825,27 +828,30 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             wt[i] = wtw[i];
-            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
+            if (tw_slot_used_wl(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
         }
         K2_STAMP(2);
         MM_MARK("M1_fwd_start");
-        fft_regs_w<LOG2N, -1>(v, t, lds, wt);
+        fft_dif<LOG2N, -1>(v, t, lds, wt);
         MM_MARK("M2_fwd_end");
         K2_STAMP(3);
         const bool pass_frame = fr == 0 && first_passthrough;
         if constexpr (blk0) {
             // packed group: Z = F0 + i FN.  Upper half of Z to LDS for the partner
-            // reads (bins fy <= N/2 live in j < 4, plus fy = N/2 at t = 0, j = 4).
+            // reads (bins fy < N/2 live in j < 4, fy = N/2 at t = 0, j = 4, in
+            // fft_bin's layout as in natural order).  First every wave leaves its
+            // fft_dif region.
+            __syncthreads();
             if (packed) {
 #pragma unroll
-                for (int j = 4; j < 8; ++j) lds[pad8(t + j * T)] = v[j];
+                for (int j = 4; j < 8; ++j) lds[pad8(fft_bin<LOG2N>(t, j))] = v[j];
             }
             __syncthreads();
             if (packed) {
 #pragma unroll
                 for (int j = 0; j < 5; ++j) {
                     __builtin_amdgcn_sched_barrier(0);
-                    const int fy = t + j * T;
+                    const int fy = fft_bin<LOG2N>(t, j);
                     if (j < 4 || fy == N / 2) {
                         // partner Z[N - fy]: upper half (fy = 0, N/2 pair with themselves)
                         const c2 z = v[j];
@@ -870,7 +876,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             if (packed && !pass_frame) {
 #pragma unroll
                 for (int j = 4; j < 8; ++j) {
-                    const int fy = t + j * T;
+                    const int fy = fft_bin<LOG2N>(t, j);
                     if (fy != N / 2) v[j] = lds[pad8(N - fy)];
                 }
             }
@@ -889,7 +895,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
-                const int fy = t + j * T;
+                const int fy = fft_bin<LOG2N>(t, j);
                 const c2 a = pyramid_op_1band(v[j], prev[j], sp, tab0[fy <= N / 2 ? fy : N - fy]);
                 prev[j] = v[j];
                 v[j] = a;
@@ -900,7 +906,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             for (int j = 0; j < 8; ++j) {
                 // one bin at a time: keeps the 8 op instances from being interleaved
                 __builtin_amdgcn_sched_barrier(0);
-                const c2 a = k2_op<LOG2N, MODE>(v[j], prev[j], f, t + j * T, sp, tab0);
+                const c2 a = k2_op<LOG2N, MODE>(v[j], prev[j], f, fft_bin<LOG2N>(t, j), sp, tab0);
                 prev[j] = v[j];
                 v[j] = a;
             }
@@ -908,15 +914,15 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         }
         K2_STAMP(4);
         MM_MARK("M3_inv_start");
-        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
+        fft_dit<LOG2N, +1>(v, t, lds, wt);   // natural row order again
         MM_MARK("M4_inv_end");
         K2_STAMP(5);
+        __syncthreads();   // every wave past its exchange reads: the staging overwrites them
         // Q is stored by row pairs (q_index) so that K3 reads each of its two
         // rows' values as one 16-B piece per bin, contiguous across the wave (a
         // column-major Q made K3's 16-B gathers cost it 4 of its 7 us/frame at
         // 1080p).  The GPW columns of the workgroup are transposed through LDS
-        // (over the exchange buffers: every group has passed the barrier after
-        // its last exchange read) and leave as one contiguous GPW*16-byte piece
+        // (over the exchange buffers) and leave as one contiguous GPW*16-byte piece
         // per row pair; same-XCD workgroups complete the 128-B lines.
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -949,7 +955,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             // thread) is mirrored the same way.
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
-                const int fy = t0 + j * T;
+                const int fy = fft_bin<LOG2N>(t0, j);
                 if (j < 4 || fy == N / 2) {
                     state_out[fy] = prev[j];
                     const c2 n = ldsN[fy];
@@ -962,7 +968,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + t0 + j * T] = prev[j];
+            for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + fft_bin<LOG2N>(t0, j)] = prev[j];
         }
     }
 }

@@ -9,6 +9,14 @@
  *   mm_cli [-w W] [-h H] [-n frames] [-l levels] [-s phase_scale]
  *          [-b frames_per_call] [-i in.{rgba,y4m}] [-o out.{rgba,y4m}] [-d device]
  *          [--full-range] [--standard] [--show-magnitude] [--show-phase]
+ *          [--checksum] [--ring-world G --ring-rank R --ring-id FILE]
+ *
+ * --ring-*: frame-sharded synthetic stream over an RCCL ring (include/mm_ring.h,
+ * SURVEY.md §8e), one process per GPU: rank R of G processes chunks of -b
+ * frames, the ring carries the chunk-boundary state; rank 0 writes the ring id
+ * to FILE, the others read it.  --checksum prints "frame <t> <byte sum>" per
+ * output frame (global frame index t), so a sharded run can be compared with
+ * the single-process stream.
  *
  * .y4m input: 8-bit 4:2:0 / 4:4:4 / mono YUV4MPEG2, geometry from its header
  * (host/y4m.h, BT.601 limited range unless --full-range); .y4m output is 4:4:4
@@ -20,7 +28,11 @@
 #include <string.h>
 
 #include "mm.h"
+#include "mm_ring.h"
 #include "y4m.h"
+
+#include <time.h>
+#include <unistd.h>
 
 #define CHECK(x)                                                                      \
     do {                                                                              \
@@ -37,18 +49,117 @@ static int ends_with(const char *s, const char *suf)
     return n >= m && strcmp(s + n - m, suf) == 0;
 }
 
+static void print_checksums(const unsigned char *dev, size_t fb, int n, int t0)
+{
+    unsigned char *h = (unsigned char *)malloc(fb * (size_t)n);
+    if (!h || hipMemcpy(h, dev, fb * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) {
+        free(h);
+        return;
+    }
+    for (int k = 0; k < n; ++k) {
+        unsigned long long sum = 0;
+        for (size_t i = 0; i < fb; ++i) sum += h[fb * (size_t)k + i];
+        printf("frame %d %llu\n", t0 + k, sum);
+    }
+    free(h);
+}
+
+/* Ring id out of band: rank 0 writes FILE (atomically), the others wait for it. */
+static int ring_id(int rank, const char *path, unsigned char id[MM_RING_ID_BYTES])
+{
+    if (rank == 0) {
+        if (mm_ring_get_id(id)) return 1;
+        char tmp[4096];
+        snprintf(tmp, sizeof tmp, "%s.tmp", path);
+        FILE *f = fopen(tmp, "wb");
+        if (!f || fwrite(id, 1, MM_RING_ID_BYTES, f) != MM_RING_ID_BYTES) return 1;
+        fclose(f);
+        return rename(tmp, path) != 0;
+    }
+    for (int tries = 0; tries < 1200; ++tries) {   /* 60 s */
+        FILE *f = fopen(path, "rb");
+        if (f) {
+            const size_t got = fread(id, 1, MM_RING_ID_BYTES, f);
+            fclose(f);
+            if (got == MM_RING_ID_BYTES) return 0;
+        }
+        struct timespec ts = {0, 50 * 1000 * 1000};
+        nanosleep(&ts, NULL);
+    }
+    return 1;
+}
+
+/* Frame-sharded synthetic stream: rank R of G owns frames
+ * [s*G*B + R*B, s*G*B + (R+1)*B) of step s. */
+static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world, int rank,
+                    const char *id_path, int checksum)
+{
+    unsigned char id[MM_RING_ID_BYTES];
+    if (ring_id(rank, id_path, id)) {
+        fprintf(stderr, "ring id exchange through %s failed\n", id_path);
+        return 1;
+    }
+    mm_ring *r = NULL;
+    int rc = mm_ring_create(world, rank, id, dev, h, W, H, B, MM_RGBA8, &r);
+    if (rc) {
+        fprintf(stderr, "mm_ring_create: %s (%s)\n", mm_strerror(rc), mm_ring_last_error());
+        return 1;
+    }
+    const size_t fb = (size_t)W * H * 4;
+    void *d_in = NULL, *d_out = NULL, *d_next = NULL;
+    if (hipMalloc(&d_in, fb * B) != hipSuccess || hipMalloc(&d_out, fb * B) != hipSuccess ||
+        hipMalloc(&d_next, fb) != hipSuccess) {
+        fprintf(stderr, "hipMalloc failed\n");
+        return 1;
+    }
+    hipStream_t s = (hipStream_t)mm_stream(h);
+    const int steps = F / (world * B);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    double t_proc = 0.0;
+    for (int st = 0; st < steps; ++st) {
+        const int t0 = st * world * B + rank * B;
+        CHECK(mm_synth_frames(d_in, W, H, t0, B, 0x5EED0000ull, 0, s));
+        const int last = st + 1 < steps;
+        if (last) CHECK(mm_synth_frames(d_next, W, H, t0 + world * B + B - 1, 1, 0x5EED0000ull, 0, s));
+        hipEventRecord(e0, s);
+        rc = mm_ring_step(r, st, d_in, d_out, last ? d_next : NULL, s);
+        if (rc) {
+            fprintf(stderr, "mm_ring_step: %s (%s)\n", mm_strerror(rc), mm_ring_last_error());
+            return 1;
+        }
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (st > 0) t_proc += ms * 1e-3;
+        if (checksum) print_checksums((const unsigned char *)d_out, fb, B, t0);
+    }
+    if (steps > 1 && t_proc > 0)
+        printf("rank %d/%d  steps %d  frames/s per rank %.1f\n", rank, world, steps,
+               (steps - 1) * B / t_proc);
+    mm_ring_destroy(r);
+    hipFree(d_in);
+    hipFree(d_out);
+    hipFree(d_next);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     int W = 1920, H = 1080, F = 300, L = 5, B = 30, dev = 0;
-    int full_range = 0, standard = 0, show_mag = 0, show_phase = 0;
+    int full_range = 0, standard = 0, show_mag = 0, show_phase = 0, checksum = 0;
+    int ring_world = 0, ring_rank = 0;
     float S = 25.0f;
-    const char *in_path = NULL, *out_path = NULL;
+    const char *in_path = NULL, *out_path = NULL, *ring_id_path = NULL;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         if (!strcmp(a, "--full-range")) { full_range = 1; continue; }
         if (!strcmp(a, "--standard")) { standard = 1; continue; }
         if (!strcmp(a, "--show-magnitude")) { show_mag = 1; continue; }
         if (!strcmp(a, "--show-phase")) { show_phase = 1; continue; }
+        if (!strcmp(a, "--checksum")) { checksum = 1; continue; }
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
         if (!v) { fprintf(stderr, "missing value for %s\n", a); return 2; }
         if (!strcmp(a, "-w")) W = atoi(v);
@@ -60,6 +171,9 @@ int main(int argc, char **argv)
         else if (!strcmp(a, "-d")) dev = atoi(v);
         else if (!strcmp(a, "-i")) in_path = v;
         else if (!strcmp(a, "-o")) out_path = v;
+        else if (!strcmp(a, "--ring-world")) ring_world = atoi(v);
+        else if (!strcmp(a, "--ring-rank")) ring_rank = atoi(v);
+        else if (!strcmp(a, "--ring-id")) ring_id_path = v;
         else { fprintf(stderr, "unknown option %s\n", a); return 2; }
         ++i;
     }
@@ -89,6 +203,16 @@ int main(int argc, char **argv)
     int N = 0;
     mm_padded_size(h, &N);
     printf("Original: %dx%d, Padded: %dx%d\n", W, H, N, N);   /* .cs:304 */
+    if (ring_world > 0) {
+        if (!ring_id_path || fi || fo) {
+            fprintf(stderr, "--ring-world needs --ring-id and a synthetic stream\n");
+            return 2;
+        }
+        CHECK(mm_set_batch(h, B));
+        const int rc = run_ring(h, W, H, F, B, dev, ring_world, ring_rank, ring_id_path, checksum);
+        mm_destroy(h);
+        return rc;
+    }
 
     const size_t fb = (size_t)W * H * 4;
     void *d_in = NULL, *d_out = NULL;
@@ -141,6 +265,7 @@ int main(int argc, char **argv)
         float ms = 0.0f;
         hipEventElapsedTime(&ms, e0, e1);
         if (done > 0) t_proc += ms * 1e-3;      /* first call holds the passthrough frame */
+        if (checksum) print_checksums((const unsigned char *)d_out, fb, n, done);
         if (fo) {
             hipMemcpy(host, d_out, fb * n, hipMemcpyDeviceToHost);
             if (y4m_out) {

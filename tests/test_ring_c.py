@@ -1,0 +1,72 @@
+"""The C ring (include/mm_ring.h, host/mm_ring.c): frame-sharded streaming with
+one RCCL ncclSend/ncclRecv per step, driven by the C host (mm_cli --ring-*).
+
+CPU: the library loads, links RCCL and exports every symbol mm_ring.h declares.
+GPU: at world 1 the ring shifts the state to and from the same rank through
+RCCL every step; the output must be bitwise the single-process stream (the
+multi-rank RCCL path runs only on an 8-GPU node: a box here has one GPU, and
+RCCL refuses two ranks on one device).
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "phase-based-motion-manipulation_amd")
+LIB = os.path.join(PKG, "lib", "libmm_ring.so")
+CLI = os.path.join(PKG, "bin", "mm_cli")
+HDR = os.path.join(ROOT, "include", "mm_ring.h")
+
+
+def header_symbols():
+    txt = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(mm_ring_[a-z_]+)\s*\(", txt)))
+
+
+def test_ring_library_exports_header_symbols():
+    syms = header_symbols()
+    assert syms == ["mm_ring_create", "mm_ring_destroy", "mm_ring_get_id", "mm_ring_last_error",
+                    "mm_ring_step"]
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(syms) <= exported
+    deps = subprocess.run(["ldd", LIB], capture_output=True, text=True, check=True).stdout
+    assert "librccl" in deps and "libmm355" in deps
+
+
+def test_ring_rejects_bad_arguments_without_gpu():
+    import ctypes
+    L = ctypes.CDLL(LIB)
+    L.mm_ring_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    out = ctypes.c_void_p()
+    idb = (ctypes.c_ubyte * 128)()
+    assert L.mm_ring_create(1, 0, idb, 0, None, 64, 48, 4, 0, ctypes.byref(out)) == -1
+    assert L.mm_ring_create(0, 0, idb, 0, None, 64, 48, 4, 0, ctypes.byref(out)) == -1
+    L.mm_ring_step.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_void_p]
+    assert L.mm_ring_step(None, 0, None, None, None, None) == -1
+
+
+def _checksums(txt):
+    return [(int(a), int(b)) for a, b in re.findall(r"^frame (\d+) (\d+)$", txt, flags=re.M)]
+
+
+@pytest.mark.gpu
+def test_c_ring_world1_equals_single_stream(tmp_path):
+    """mm_cli --ring-world 1: 4 steps of 12 frames at 256x144 through the RCCL
+    self-ring == mm_cli over the same 48 frames in one process (bitwise)."""
+    common = ["-w", "256", "-h", "144", "-n", "48", "-b", "12", "-l", "5", "-s", "25", "--checksum"]
+    env = dict(os.environ, NCCL_DEBUG="WARN")
+    one = subprocess.run([CLI] + common, capture_output=True, text=True, timeout=120, env=env)
+    assert one.returncode == 0, one.stderr
+    ring = subprocess.run([CLI] + common + ["--ring-world", "1", "--ring-rank", "0",
+                                            "--ring-id", str(tmp_path / "ring.id")],
+                          capture_output=True, text=True, timeout=180, env=env)
+    assert ring.returncode == 0, ring.stdout + ring.stderr
+    a, b = _checksums(one.stdout), _checksums(ring.stdout)
+    assert len(a) == 48 and a == b
