@@ -619,19 +619,22 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 {
     return (size_t)k2_groups<LOG2N>() *
                (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_entries<LOG2N>()) +
-           sizeof(float2) * k2_tab_entries<LOG2N>() + sizeof(c2) * ((1 << LOG2N) / 2 + 1) +
-           sizeof(float) * (1 << LOG2N);
+           sizeof(float2) * k2_tab_entries<LOG2N>() + sizeof(c2) * 2 + sizeof(float) * (1 << LOG2N);
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
 // f = N/2 (row DFT bins that are real for real rows, so their column spectra are
-// Hermitian in fy) share group 0 of block 0 as one complex column z = G0 + i*GN:
-// the op runs on fy <= N/2 for both and the upper half is mirrored, through the
-// exchange buffer: the upper half of Z is stored for the partner reads
-// Z[N - fy], and the mirrored A goes into the (unused) lower half.  The
-// grid is then exactly N/2 groups (512 two-column workgroups at N=2048: one
-// resident round at 2 WGs/CU, no one-group tail).  Column N/2's F_{t-1} stays
-// in LDS (ldsN) across the frames of a launch.
+// Hermitian in fy) share group 0 of block 0 as one complex column z = G0 + i*GN.
+// The grid is then exactly N/2 groups (512 two-column workgroups at N=2048: one
+// resident round at 2 WGs/CU, no one-group tail).  After the forward FFT the
+// packed group unpacks F0, FN from Z(fy), Z(N-fy) (partner bins through LDS)
+// and runs the same number of ops per thread as any other group: a thread's
+// bins fy < N/2 (j < 4) carry column 0's op at fy, its bins fy > N/2 carry
+// column N/2's op at N - fy, and thread 0 alone adds the two real bins of
+// column N/2 (0 and N/2).  Its F_{t-1} registers hold those same bins (FN(0),
+// FN(N/2) in ldsX).  A second exchange recombines A = A0 + i AN per bin.
+// (The packed block is the kernel's critical path: every block is resident at
+// once, so its extra work is the kernel's.)
 #ifndef MM_K2_OPG
 #define MM_K2_OPG 8   // bins of the branch-free op interleaved per scheduling group
 #endif
@@ -668,11 +671,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     c2 *lds = lds_all + grp * lds_complex<N>();
     float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TE;
     float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TE;
-    // column N/2: F_{t-1} at bins 0..N/2 between frames, and one frame's Q
-    // values by list row (staged like the others: no global round trip and no
-    // store the next frame's loads must wait for)
-    c2 *ldsN = reinterpret_cast<c2 *>(tabN + TE);
-    float *stgN = reinterpret_cast<float *>(ldsN + N / 2 + 1);
+    // column N/2: F_{t-1} at its real bins 0 and N/2 (thread 0 of the packed
+    // group), and one frame's Q values by list row (staged like the others: no
+    // global round trip and no store the next frame's loads must wait for)
+    c2 *ldsX = reinterpret_cast<c2 *>(tabN + TE);
+    float *stgN = reinterpret_cast<float *>(ldsX + 2);
     const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
@@ -696,27 +699,31 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 
     // waves whose bins all have at most one middle band (frame-invariant,
     // uniform) take the branch-free op
+    // packed group: bin j's op column (0 or N/2) and bin within it
+    auto pk_col0 = [&](int j, int fy) { return j < 4 || fy == N / 2; };
     bool wave_two_band = true;
     if constexpr (MODE == MM_K2_PYR_TAB) {
         bool two = false;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int fy = fft_bin<LOG2N>(t0, j);
-            two |= !__builtin_signbit(tab0[fy <= N / 2 ? fy : N - fy].y);
+            if (packed && !pk_col0(j, fy)) two |= !__builtin_signbit(tabN[N - fy].y);
+            else two |= !__builtin_signbit(tab0[fy <= N / 2 ? fy : N - fy].y);
         }
+        if (packed && t0 == 0)
+            two |= !__builtin_signbit(tabN[0].y) || !__builtin_signbit(tabN[N / 2].y);
         wave_two_band = __any(two);
     }
     c2 prev[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-        prev[j] = state_in ? state_in[(size_t)f * N + fft_bin<LOG2N>(t0, j)] : mk(0.0f, 0.0f);
-    if (packed) {   // each thread reads and writes only its own bins: no barrier
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int fy = fft_bin<LOG2N>(t0, j);
-            if (j < 4 || fy == N / 2)
-                ldsN[fy] = state_in ? state_in[(size_t)(N / 2) * N + fy] : mk(0.0f, 0.0f);
-        }
+    for (int j = 0; j < 8; ++j) {
+        const int fy = fft_bin<LOG2N>(t0, j);
+        const size_t at = packed && !pk_col0(j, fy) ? (size_t)(N / 2) * N + (N - fy) : (size_t)f * N + fy;
+        prev[j] = state_in ? state_in[at] : mk(0.0f, 0.0f);
+    }
+    if (packed && t0 == 0) {   // FN(0), FN(N/2): thread 0's alone, no barrier
+        ldsX[0] = state_in ? state_in[(size_t)(N / 2) * N] : mk(0.0f, 0.0f);
+        ldsX[1] = state_in ? state_in[(size_t)(N / 2) * N + N / 2] : mk(0.0f, 0.0f);
     }
 
     // G column of a frame.  Rows outside the image get an out-of-range buffer
@@ -769,6 +776,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #ifdef MM_K2_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+    st_acc[7] = __builtin_amdgcn_s_memrealtime();   // loop start (100 MHz, device-wide)
 #endif
     for (int fr = 0;; ++fr) {
         // Opaque per-iteration copy of the lane index: stops LICM from hoisting
@@ -776,6 +784,14 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         // loop (that pinned ~200 VGPRs and capped occupancy at 1 wave/SIMD).
         int t = t0;
         asm volatile("" : "+v"(t));
+        // Two workgroups share a CU for the whole launch and the SIMD arbiter
+        // favours the older one (issue priority, then age): it ran ahead and
+        // left the younger one alone for the last third (phase stamps: loop
+        // times 917 vs 1357 us per 100 frames).  Alternating the priority
+        // every frame between the first-dispatched half of the grid and the
+        // second keeps a pair in step (1082..1305 us).
+        if ((fr ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
         load_g(fr < nframes ? fr : nframes - 1, t);
         K2_STAMP(0);
         __builtin_amdgcn_sched_barrier(0);   // keep the stores behind the loads
@@ -836,82 +852,129 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         MM_MARK("M2_fwd_end");
         K2_STAMP(3);
         const bool pass_frame = fr == 0 && first_passthrough;
-        if constexpr (blk0) {
-            // packed group: Z = F0 + i FN.  Upper half of Z to LDS for the partner
-            // reads (bins fy < N/2 live in j < 4, fy = N/2 at t = 0, j = 4, in
-            // fft_bin's layout as in natural order).  First every wave leaves its
-            // fft_dif region.
-            __syncthreads();
-            if (packed) {
+        // the spectral op of a regular group (all groups but the packed one)
+        auto regular_op = [&]() {
+            if (pass_frame) {
 #pragma unroll
-                for (int j = 4; j < 8; ++j) lds[pad8(fft_bin<LOG2N>(t, j))] = v[j];
-            }
-            __syncthreads();
-            if (packed) {
+                for (int j = 0; j < 8; ++j) prev[j] = v[j];
+            } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
+                // no bin of this wave has two middle bands: branch-free op, bins
+                // interleaved MM_K2_OPG at a time
 #pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    __builtin_amdgcn_sched_barrier(0);
+                for (int j = 0; j < 8; ++j) {
+                    if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
                     const int fy = fft_bin<LOG2N>(t, j);
-                    if (j < 4 || fy == N / 2) {
-                        // partner Z[N - fy]: upper half (fy = 0, N/2 pair with themselves)
-                        const c2 z = v[j];
-                        const c2 zm = (fy == 0 || fy == N / 2) ? z : lds[pad8(N - fy)];
-                        const c2 f0 = mk(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-                        const c2 fN = mk(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
-                        if (!pass_frame) {
-                            const c2 pn = ldsN[fy];
-                            const c2 a0 = k2_op<LOG2N, MODE>(f0, prev[j], 0, fy, sp, tab0);
-                            const c2 an = k2_op<LOG2N, MODE>(fN, pn, N / 2, fy, sp, tabN);
-                            v[j] = mk(a0.x - an.y, a0.y + an.x);   // A0 + i AN
-                            if (j < 4)   // bin N - fy reads conj(A0) + i conj(AN)
-                                lds[pad8(fy)] = mk(a0.x + an.y, an.x - a0.y);
-                        }
-                        prev[j] = f0;
-                        ldsN[fy] = fN;
-                    }
+                    const c2 a = pyramid_op_1band(v[j], prev[j], sp, tab0[fy <= N / 2 ? fy : N - fy]);
+                    prev[j] = v[j];
+                    v[j] = a;
                 }
                 __builtin_amdgcn_sched_barrier(0);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    // one bin at a time: keeps the 8 op instances from being interleaved
+                    __builtin_amdgcn_sched_barrier(0);
+                    const c2 a = k2_op<LOG2N, MODE>(v[j], prev[j], f, fft_bin<LOG2N>(t, j), sp, tab0);
+                    prev[j] = v[j];
+                    v[j] = a;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        if constexpr (blk0) {
+            // packed group (see above the kernel).  First every wave leaves its
+            // fft_dif region; then Z of every bin to LDS for the partner reads.
+            __syncthreads();
+            if (packed) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) lds[pad8(fft_bin<LOG2N>(t, j))] = v[j];
+            }
+            __syncthreads();
+            // v[j] becomes A0(fy) (j < 4) / AN(N - fy) (j >= 4)
+            c2 an0 = mk(0.0f, 0.0f), anh = mk(0.0f, 0.0f);   // thread 0: AN(0), AN(N/2)
+            if (packed) {
+                // unpack every bin (partner Z(N - fy) from LDS), then the ops
+                c2 fn0 = mk(0.0f, 0.0f), fnh = mk(0.0f, 0.0f);   // thread 0: FN(0), FN(N/2)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int fy = fft_bin<LOG2N>(t, j);
+                    const c2 z = v[j], m = lds[pad8((N - fy) & (N - 1))];
+                    const c2 f0 = mk(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));    // F0(fy)
+                    const c2 fn = mk(0.5f * (z.y + m.y), -0.5f * (z.x - m.x));   // FN(fy)
+                    v[j] = pk_col0(j, fy) ? f0 : mk(fn.x, -fn.y);                // or FN(N - fy)
+                    if (j == 0) fn0 = fn;
+                    if (j == 4) fnh = fn;
+                }
+                if (!pass_frame) {
+                    if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
+                            const int fy = fft_bin<LOG2N>(t, j);
+                            const c2 c = v[j];
+                            v[j] = pyramid_op_1band(c, prev[j], sp, pk_col0(j, fy) ? tab0[fy] : tabN[N - fy]);
+                            prev[j] = c;
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            const int fy = fft_bin<LOG2N>(t, j);
+                            const c2 c = v[j];
+                            v[j] = pk_col0(j, fy) ? k2_op<LOG2N, MODE>(c, prev[j], 0, fy, sp, tab0)
+                                                  : k2_op<LOG2N, MODE>(c, prev[j], N / 2, N - fy, sp, tabN);
+                            prev[j] = c;
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (t == 0) {   // column N/2's real bins 0 and N/2
+                        an0 = k2_op<LOG2N, MODE>(fn0, ldsX[0], N / 2, 0, sp, tabN);
+                        anh = k2_op<LOG2N, MODE>(fnh, ldsX[1], N / 2, N / 2, sp, tabN);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) prev[j] = v[j];
+                }
+                if (t == 0) {
+                    ldsX[0] = fn0;
+                    ldsX[1] = fnh;
+                }
+            } else {
+                regular_op();   // the block's other group, between the same barriers
+            }
+            __syncthreads();   // partner reads of Z done: the buffer takes the ops
+            // A0 at pad8(fy), AN at LN + fy (fy <= N/2)
+            constexpr int LN = lds_complex<N>() - (N / 2 + 1);
+            if (packed && !pass_frame) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int fy = fft_bin<LOG2N>(t, j);
+                    if (pk_col0(j, fy)) lds[pad8(fy)] = v[j];
+                    else lds[LN + N - fy] = v[j];
+                }
             }
             __syncthreads();
             if (packed && !pass_frame) {
 #pragma unroll
-                for (int j = 4; j < 8; ++j) {
+                for (int j = 0; j < 8; ++j) {
                     const int fy = fft_bin<LOG2N>(t, j);
-                    if (fy != N / 2) v[j] = lds[pad8(N - fy)];
+                    c2 a0, an;
+                    if (pk_col0(j, fy)) {   // A(fy) = A0(fy) + i AN(fy)
+                        a0 = v[j];
+                        an = fy == 0 ? an0 : (fy == N / 2 ? anh : lds[LN + fy]);
+                    } else {                // A(fy) = conj A0(N-fy) + i conj AN(N-fy)
+                        const c2 b = lds[pad8(N - fy)];
+                        a0 = mk(b.x, -b.y);
+                        an = mk(v[j].x, -v[j].y);
+                    }
+                    v[j] = mk(a0.x - an.y, a0.y + an.x);
                 }
             }
             __syncthreads();   // the inverse FFT rewrites the buffer
         }
+        if constexpr (!blk0) regular_op();
         staged = !pass_frame;
-        if (pass_frame) {
-            if (!packed) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) prev[j] = v[j];
-            }
-        } else {
-        if (!packed && MODE == MM_K2_PYR_TAB && !wave_two_band) {
-            // no bin of this wave has two middle bands: branch-free op, bins
-            // interleaved MM_K2_OPG at a time
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
-                const int fy = fft_bin<LOG2N>(t, j);
-                const c2 a = pyramid_op_1band(v[j], prev[j], sp, tab0[fy <= N / 2 ? fy : N - fy]);
-                prev[j] = v[j];
-                v[j] = a;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        } else if (!packed) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                // one bin at a time: keeps the 8 op instances from being interleaved
-                __builtin_amdgcn_sched_barrier(0);
-                const c2 a = k2_op<LOG2N, MODE>(v[j], prev[j], f, fft_bin<LOG2N>(t, j), sp, tab0);
-                prev[j] = v[j];
-                v[j] = a;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        if (!pass_frame) {
         K2_STAMP(4);
         MM_MARK("M3_inv_start");
         fft_dit<LOG2N, +1>(v, t, lds, wt);   // natural row order again
@@ -942,6 +1005,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         K2_STAMP(6);
     }
 #ifdef MM_K2_STAMPS
+    st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
     if (threadIdx.x % 64 == 0) {
         const int w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
         for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
@@ -949,22 +1013,25 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #endif
     if (valid) {
         if (packed) {
-            // column 0: bins fy <= N/2 in prev[0..4]; the rest is the Hermitian
-            // mirror (bitwise: F0[N-fy] = conj F0[fy] by the unpack formula).
-            // Column N/2 (from ldsN, rows fy <= N/2 written by this same
-            // thread) is mirrored the same way.
+            // column 0 from bins fy <= N/2 (j < 4, and N/2 at thread 0), column
+            // N/2 from bins N - fy (j >= 4) and thread 0's two real bins; the
+            // other halves are the Hermitian mirrors (bitwise: the unpack gives
+            // F[N-fy] = conj F[fy]).
 #pragma unroll
-            for (int j = 0; j < 5; ++j) {
+            for (int j = 0; j < 8; ++j) {
                 const int fy = fft_bin<LOG2N>(t0, j);
-                if (j < 4 || fy == N / 2) {
-                    state_out[fy] = prev[j];
-                    const c2 n = ldsN[fy];
-                    stN[fy] = n;
-                    if (fy != 0 && fy != N / 2) {
-                        state_out[N - fy] = mk(prev[j].x, -prev[j].y);
-                        stN[N - fy] = mk(n.x, -n.y);
-                    }
+                const c2 p = prev[j], pc = mk(p.x, -p.y);
+                if (pk_col0(j, fy)) {
+                    state_out[fy] = p;
+                    if (fy != 0 && fy != N / 2) state_out[N - fy] = pc;
+                } else {
+                    stN[N - fy] = p;
+                    stN[fy] = pc;
                 }
+            }
+            if (t0 == 0) {
+                stN[0] = ldsX[0];
+                stN[N / 2] = ldsX[1];
             }
         } else {
 #pragma unroll

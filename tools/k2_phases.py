@@ -33,7 +33,10 @@ nw = 4096
 buf = (ctypes.c_ulonglong * (nw * 8))()
 L.mm_debug_k2_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 assert L.mm_debug_k2_stamps(buf, nw * 8) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8)[:, :len(PHASES)].astype(np.float64) / n
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8)
+a = raw[:, :len(PHASES)].astype(np.float64) / n
+start = (raw[:, 7] & 0xffffffff).astype(np.int64)      # loop start, 100 MHz ticks (low 32 bits)
+dur = (raw[:, 7] >> 32).astype(np.float64) * 10.0        # loop duration, ns
 waves = (h.N // 2 + 1) // 2 * 8 if False else nw
 live = a[a.sum(axis=1) > 0]
 res = {"frames": n, "waves": int(live.shape[0]),
@@ -41,4 +44,16 @@ res = {"frames": n, "waves": int(live.shape[0]),
        "cycles_per_frame_block0": {p: round(float(a[:8, i].mean()), 1) for i, p in enumerate(PHASES)},
        "total_mean": round(float(live.sum(axis=1).mean()), 1),
        "total_max": round(float(live.sum(axis=1).max()), 1)}
+tot = a.sum(axis=1)
+blk = np.arange(nw) // 8
+bt = np.array([tot[blk == b].max() for b in range(nw // 8)])
+res["block_total_pct"] = {q: round(float(np.percentile(bt, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
+res["slowest_blocks"] = [int(b) for b in np.argsort(-bt)[:8]]
+res["per_xcd_mean_total"] = [round(float(bt[np.arange(nw // 8) % 8 == x].mean()), 1) for x in range(8)]
+s0 = start - start.min()
+res["loop_start_skew_us"] = {q: round(float(np.percentile(s0, q)) / 100.0, 2) for q in (0, 50, 90, 100)}
+res["loop_duration_us"] = {q: round(float(np.percentile(dur, q)) / 1e3, 1) for q in (0, 50, 90, 100)}
+res["end_us_max"] = round(float((s0 * 10 + dur).max()) / 1e3, 1)
 print(json.dumps(res))
+if len(sys.argv) > 2:
+    np.save(sys.argv[2], raw)
