@@ -3,10 +3,10 @@
 
 Workload (BASELINE.json configs[1]): a synthetic 1920x1080 RGBA8 stream,
 5-level pyramid, PhaseScale 25, pyramid mode with orientations = 1 (the
-reference's semantics).  One STEP = one pass of the hot path over one batch of
-`--frames-per-step` consecutive frames of the stream per GPU (default 100, so
-the default 3 timed steps are the 300-frame stream of the config).  Input
-frames are generated on the device and resident in HBM before timing.
+reference's semantics).  One STEP = one mm_process_stream call over the
+config's 300-frame stream per GPU (`--frames-per-step`), processed in batches
+of 100 frames (`--batch`, mm_set_batch).  Input frames are generated on the
+device and resident in HBM before timing.
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): the stream is
 frame-sharded: each step rank g processes its own contiguous
@@ -65,7 +65,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames-per-step", type=int, default=100)
+    ap.add_argument("--frames-per-step", type=int, default=300,
+                    help="frames per step and GPU: one mm_process_stream call over the "
+                         "config's 300-frame stream by default")
+    ap.add_argument("--batch", type=int, default=100,
+                    help="frames per K1/K2/K3/K4 batch inside a step (mm_set_batch; 0: the "
+                         "whole step)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--levels", type=int, default=5)
@@ -385,7 +390,8 @@ def main():
     per_frame = a.call_pattern == "per-frame"
     # one step = one batch: K2 keeps F_{t-1} on chip across it; the per-frame
     # pattern is the reference's one OnRenderImage per frame (batch 1)
-    h.set_batch(1 if per_frame else C)
+    B = 1 if per_frame else min(a.batch or C, C)
+    h.set_batch(B)
     N = h.N
 
     # resident inputs: one buffer per step (warmup + timed), generated on device
@@ -490,7 +496,7 @@ def main():
         except Exception:
             valu = None
     B = survey_bytes_per_frame(W, H, N)
-    batch = 1 if per_frame else C
+    batch = B
 
     result = {
         "metric": metric_name(W, H, a.levels, a.orientations, a.standard), "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
@@ -506,7 +512,7 @@ def main():
                                 f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)"),
                    "frames_per_step_per_gpu": C, "padded_n": N,
                    "call_pattern": ("one mm_process per frame (batch 1)" if per_frame else
-                                    f"mm_process_stream, batch {C} frames per call"),
+                                    f"mm_process_stream, {C} frames per call in batches of {B}"),
                    "parallelism": ("single GPU" if world == 1 else
                                    f"frame-sharded x{world}, "
                                    + ("gloo rehearsal, ring state via host" if gloo

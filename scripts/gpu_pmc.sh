@@ -3,8 +3,8 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; TAG=${1:-pmc}
 export TMPDIR=/tmp
-FPS=100   # frames per K2 launch = bench.py frames per step
-B="python3 $R/bench.py --no-cpu-baseline --drop-in-frames 0 --steps 2 --warmup 1 --frames-per-step $FPS"
+FPS=100   # frames per K2 launch = bench.py batch
+B="python3 $R/bench.py --no-cpu-baseline --drop-in-frames 0 --steps 1 --warmup 1 --frames-per-step 300 --batch $FPS"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C -d $R/gpurun_out/${TAG}_$C -o run --output-format csv -- $B > /dev/null 2> gpurun_out/${TAG}_$C.err || { echo PMC $C FAIL; tail gpurun_out/${TAG}_$C.err; exit 1; }
   timeout -k 10 120 rocprofv3 --pmc $C -d $R/gpurun_out/${TAG}_cal_$C -o run --output-format csv -- $R/tools/bin/pmc_calib > /dev/null 2> gpurun_out/${TAG}_cal_$C.err || { echo CAL $C FAIL; exit 1; }
