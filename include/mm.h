@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 5
+#define MM_ABI_VERSION 6
 
 /* error codes */
 #define MM_OK               0
@@ -162,6 +162,21 @@ void *mm_stream(mm_handle *h);
  * device); call between frames.  Since ABI 5. */
 int mm_set_batch(mm_handle *h, int frames);
 int mm_get_batch(const mm_handle *h, int *frames);
+
+/* Zero-copy frames (f4): device memory owned by another API — an engine's
+ * render target exported as an opaque POSIX fd (Vulkan VK_KHR_external_memory_fd,
+ * or a HIP VMM allocation via hipMemExportToShareableHandle) — imported into the
+ * handle's device (hipImportExternalMemory) and mapped as a device pointer that
+ * mm_process / mm_process_stream take with MM_FRAMES_ON_DEVICE, in place: no
+ * staging copy, no PCIe transfer (the reference's OnRenderImage works on the
+ * engine's RenderTextures, .cs:101).  `bytes` = the exported allocation's
+ * size, `offset` = where the frames start in it.  On success the fd belongs to
+ * the import (do not close it).  Release before the exporter frees the memory.
+ * Since ABI 6. */
+typedef struct mm_ext_frames mm_ext_frames;
+int mm_import_frames(mm_handle *h, int fd, size_t bytes, size_t offset, mm_ext_frames **out);
+void *mm_ext_frames_ptr(const mm_ext_frames *x);
+int mm_release_frames(mm_ext_frames *x);
 
 /* OnDestroy/ReleaseResources (.cs:96-99, :344-356). */
 void mm_destroy(mm_handle *h);

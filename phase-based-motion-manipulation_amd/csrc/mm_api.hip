@@ -1069,6 +1069,57 @@ int mm_profile_end(mm_handle *h, double *ms, int *launches, int *frames)
     return rc;
 }
 
+struct mm_ext_frames {
+    hipExternalMemory_t mem;
+    void *ptr;
+    int device;
+};
+
+int mm_import_frames(mm_handle *h, int fd, size_t bytes, size_t offset, mm_ext_frames **out)
+{
+    if (!out) return MM_ERR_INVALID;
+    *out = nullptr;
+    if (!h || fd < 0 || bytes == 0 || offset >= bytes) return MM_ERR_INVALID;
+    DEVICE_SCOPE(h);
+    mm_ext_frames *x = new (std::nothrow) mm_ext_frames();
+    if (!x) return MM_ERR_OOM;
+    x->device = h->device;
+    hipExternalMemoryHandleDesc hd;
+    memset(&hd, 0, sizeof(hd));
+    hd.type = hipExternalMemoryHandleTypeOpaqueFd;
+    hd.handle.fd = fd;
+    hd.size = bytes;
+    if (hipImportExternalMemory(&x->mem, &hd) != hipSuccess) {
+        delete x;
+        return MM_ERR_HIP;
+    }
+    hipExternalMemoryBufferDesc bd;
+    memset(&bd, 0, sizeof(bd));
+    bd.offset = offset;
+    bd.size = bytes - offset;
+    if (hipExternalMemoryGetMappedBuffer(&x->ptr, x->mem, &bd) != hipSuccess) {
+        (void)hipDestroyExternalMemory(x->mem);
+        delete x;
+        return MM_ERR_HIP;
+    }
+    *out = x;
+    return MM_OK;
+}
+
+void *mm_ext_frames_ptr(const mm_ext_frames *x) { return x ? x->ptr : nullptr; }
+
+int mm_release_frames(mm_ext_frames *x)
+{
+    if (!x) return MM_ERR_INVALID;
+    DeviceScope dev_scope_(x->device);
+    int rc = MM_OK;
+    if (hipDeviceSynchronize() != hipSuccess) rc = MM_ERR_HIP;   // in-flight work may use them
+    if (hipFree(x->ptr) != hipSuccess) rc = MM_ERR_HIP;
+    if (hipDestroyExternalMemory(x->mem) != hipSuccess) rc = MM_ERR_HIP;
+    delete x;
+    return rc;
+}
+
 int mm_synth_frames(void *dev_out, int width, int height, int t0, int count, uint64_t seed,
                     int gray, void *hip_stream)
 {

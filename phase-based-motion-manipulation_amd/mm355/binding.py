@@ -74,7 +74,7 @@ class Params(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 5   # include/mm.h MM_ABI_VERSION
+ABI_VERSION = 6   # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):
@@ -111,6 +111,9 @@ def load_library(path=None):
         "mm_synth_frames": (ci, [vp, ci, ci, ci, ci, ctypes.c_uint64, ci, vp]),
         "mm_resample_table": (ci, [ci, ci, ci, ci, ctypes.POINTER(ctypes.c_int32),
                                    ctypes.POINTER(cf)]),
+        "mm_import_frames": (ci, [vp, ci, sz, sz, ctypes.POINTER(vp)]),
+        "mm_ext_frames_ptr": (vp, [vp]),
+        "mm_release_frames": (ci, [vp]),
         "mm_profile_begin": (ci, [vp]),
         "mm_profile_end": (ci, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci),
                                 ctypes.POINTER(ci)]),
@@ -118,6 +121,8 @@ def load_library(path=None):
     abi = L.mm_abi_version()
     for name, (res, args) in sigs.items():
         if abi < 5 and name in ("mm_set_batch", "mm_get_batch"):
+            continue
+        if abi < 6 and name in ("mm_import_frames", "mm_ext_frames_ptr", "mm_release_frames"):
             continue
         fn = getattr(L, name)
         fn.restype = res

@@ -1,0 +1,37 @@
+"""Zero-copy frames (f4): memory exported by another API as a POSIX fd is
+imported with mm_import_frames and processed in place (include/mm.h, ABI 6).
+
+The exporter here is HIP's virtual-memory API (hipMemCreate with a POSIX-fd
+handle type + hipMemExportToShareableHandle), standing in for a Vulkan render
+target exported with VK_KHR_external_memory_fd: the import path is the same
+(hipImportExternalMemory, opaque fd).  bin/mm_extmem_check runs the stream
+through the imported mappings one mm_process call per frame and compares the
+output, read back through the exporter's own mapping, with the same stream
+processed from ordinary device buffers (bitwise).
+"""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import mm355
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHECK = os.path.join(ROOT, "phase-based-motion-manipulation_amd", "bin", "mm_extmem_check")
+
+
+def test_import_rejects_bad_arguments_without_gpu():
+    L = mm355.lib()
+    out = ctypes.c_void_p()
+    assert L.mm_import_frames(None, 3, 4096, 0, ctypes.byref(out)) == -1
+    assert L.mm_release_frames(None) == -1
+    assert L.mm_ext_frames_ptr(None) is None
+
+
+@pytest.mark.gpu
+def test_zero_copy_import_matches_device_buffers():
+    r = subprocess.run([CHECK, "-w", "256", "-h", "144", "-n", "8"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "extmem ok" in r.stdout
