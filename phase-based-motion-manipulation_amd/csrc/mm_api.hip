@@ -288,21 +288,26 @@ static int set_attrs(int W)
 template <int LOG2N>
 static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipStream_t s)
 {
-    const int ppf = h->H / 2;
+    const int ppf = (h->H + 1) / 2;   // odd H: the last pair's second row is zero
     const int total = ppf * nframes;
     const int gpw = k1_groups<LOG2N>();
     const int blocks = (total + gpw - 1) / gpw;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     const size_t lds = sizeof(c2) * (size_t)gpw * lds_complex<(1 << LOG2N)>();
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
-    if (fmt == MM_RGBA8)
-        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 0>), dim3(blocks), dim3(k1_threads<LOG2N>()),
-                           lds, s, in, fb, ppf, total, h->geo, h->d_col3,
-                           h->d_row3, h->d_tw, h->d_G, h->g_stride);
-    else
-        hipLaunchKernelGGL((k_rows_fwd<LOG2N, 1>), dim3(blocks), dim3(k1_threads<LOG2N>()),
-                           lds, s, in, fb, ppf, total, h->geo, h->d_col3,
-                           h->d_row3, h->d_tw, h->d_G, h->g_stride);
+#define MM_K1_LAUNCH(F, GEN)                                                              \
+    hipLaunchKernelGGL((k_rows_fwd<LOG2N, F, GEN>), dim3(blocks), dim3(k1_threads<LOG2N>()), lds, s, \
+                       in, fb, ppf, total, h->geo, h->d_col3, h->d_row3, h->d_col, h->d_row,       \
+                       h->d_tw, h->d_G, h->g_stride)
+    const bool gen = h->geo.ox || h->geo.oy;   // odd W/H: taps span i-2 .. i+1
+    if (fmt == MM_RGBA8) {
+        if (gen) MM_K1_LAUNCH(0, true);
+        else MM_K1_LAUNCH(0, false);
+    } else {
+        if (gen) MM_K1_LAUNCH(1, true);
+        else MM_K1_LAUNCH(1, false);
+    }
+#undef MM_K1_LAUNCH
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -361,6 +366,19 @@ static int launch_k4(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    if (h->geo.ox || h->geo.oy) {   // odd W/H: the crop samples between texels
+        const size_t tot = (size_t)nout * h->W * h->H;
+        ProfScope ps(h, s, MM_K_COMPOSE, nout);
+        const dim3 grid((unsigned)((tot + 255) / 256));
+        if (fmt == MM_RGBA8)
+            hipLaunchKernelGGL((k_compose_odd<0>), grid, dim3(256), 0, s, h->d_Yh, h->yh_stride, in, out,
+                               fb, frame0, nout, h->geo, h->blur, h->d_col, h->d_row);
+        else
+            hipLaunchKernelGGL((k_compose_odd<1>), grid, dim3(256), 0, s, h->d_Yh, h->yh_stride, in, out,
+                               fb, frame0, nout, h->geo, h->blur, h->d_col, h->d_row);
+        HIPCHK(hipGetLastError());
+        return MM_OK;
+    }
     const int rt = (h->H + kTileRows - 1) / kTileRows, ct = (h->W + kTileCols - 1) / kTileCols;
     const dim3 grid(rt * ct * nout);
     ProfScope ps(h, s, MM_K_COMPOSE, nout);
@@ -752,7 +770,10 @@ static std::vector<float4> merge3(const std::vector<Tap4> &tab, int edge)
     std::vector<float4> out(tab.size());
     for (int i = 0; i < n; ++i) {
         float w[3] = {0.0f, 0.0f, 0.0f};
-        for (int m = 0; m < 4; ++m) w[tab[i].idx[m] - i + 1] += tab[i].w[m];
+        for (int m = 0; m < 4; ++m) {   // non-local taps (odd sizes) use the Tap4 paths
+            const int o = tab[i].idx[m] - i + 1;
+            if (o >= 0 && o < 3) w[o] += tab[i].w[m];
+        }
         const int l = i > 0 ? i - 1 : (edge ? 0 : n - 1);
         const int r = i < n - 1 ? i + 1 : (edge ? n - 1 : 0);
         const uint32_t bits = (uint32_t)l | ((uint32_t)r << 16);
@@ -768,7 +789,9 @@ static int upload_tables(mm_handle *h)
     std::vector<Tap4> col, row;
     build_tab(h->W, h->N, h->p.edge_mode, col);
     build_tab(h->H, h->N, h->p.edge_mode, row);
-    if (!taps_local(col) || !taps_local(row)) return MM_ERR_UNSUPPORTED;  // k_compose tiling
+    // k_compose's tiling and K1's 3-tap path need taps on i-1 .. i+1; odd sizes
+    // (taps on i-2 .. i+1) take the Tap4 paths (k_rows_fwd<GEN>, k_compose_odd)
+    if (!h->geo.ox && !h->geo.oy && (!taps_local(col) || !taps_local(row))) return MM_ERR_UNSUPPORTED;
     const std::vector<float4> c3 = merge3(col, h->p.edge_mode), r3 = merge3(row, h->p.edge_mode);
     HIPCHK(hipMemcpy(h->d_col3, c3.data(), sizeof(float4) * h->W, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_row3, r3.data(), sizeof(float4) * h->H, hipMemcpyHostToDevice));
@@ -781,7 +804,10 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
 {
     if (!out) return MM_ERR_INVALID;
     *out = nullptr;
-    if (width < 2 || height < 2 || (width & 1) || (height & 1)) return MM_ERR_UNSUPPORTED;
+    if (width < 2 || height < 2) return MM_ERR_UNSUPPORTED;
+    // odd sizes: the pyramid, standard and debug paths (the steerable extension's
+    // band kernels assume integer quad offsets)
+    if (((width | height) & 1) && p && p->mode == MM_MODE_STEERABLE) return MM_ERR_UNSUPPORTED;
     int rc = validate_params(p);
     if (rc) return rc;
     const int N = next_pow2(std::max(std::max(width, height), 16));
@@ -812,7 +838,11 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.x0 = (N - width) / 2;   // PadTexture offsets (.cs:360-363)
     g.y0 = (N - height) / 2;
     g.rb = g.y0 - 2;
-    g.Hn = std::min(height + 4, N);
+    g.ox = width & 1;
+    g.oy = height & 1;
+    g.Hg = height + g.oy;
+    g.Wy = width + g.ox;
+    g.Hn = std::min(height + 4 + g.oy, N);   // + the crop's second texel row
     g.TK = q_tile_v(ilog2(N));
     g.Hq = (g.Hn + g.TK - 1) / g.TK * g.TK;
     g.Qs = N / 2 + 2;
@@ -822,9 +852,9 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->blur = build_blur();
 
     h->chunk = default_batch(width, height, N);
-    h->g_stride = (size_t)(N / 2 + 1) * height;
+    h->g_stride = (size_t)(N / 2 + 1) * g.Hg;
     h->q_stride = (size_t)g.Qs * g.Hq;
-    h->yh_stride = (size_t)g.Hn * width;
+    h->yh_stride = (size_t)g.Hq * g.Wy;   // whole Q tiles of rows: K3 stores row pairs
 
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         free_handle(h);
@@ -872,6 +902,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     if (!h) return MM_ERR_INVALID;
     int rc = validate_params(p);
     if (rc) return rc;
+    if (p->mode == MM_MODE_STEERABLE && (h->geo.ox || h->geo.oy)) return MM_ERR_UNSUPPORTED;
     const bool edge_changed = p->edge_mode != h->p.edge_mode;
     DEVICE_SCOPE(h);
     HIPCHK(hipDeviceSynchronize());   // in-flight work on any stream may read the tables

@@ -30,7 +30,12 @@ struct Tap4 {         // composite stretch+pad bilinear taps incl. Hann factor
 
 struct Geo {
     int W, H, N;
-    int x0, y0;       // image placement inside the canvas (PadTexture .cs:360-363)
+    int x0, y0;       // image placement inside the canvas (PadTexture .cs:360-363):
+                      // floor((N - W) / 2); for odd N - W the quad's left edge is at
+                      // x0 + 0.5 and CropTexture samples between two texels
+    int ox, oy;       // W, H odd (k_compose_odd)
+    int Hg;           // rows per G column (H rounded up to even: K1 writes row pairs)
+    int Wy;           // Yh columns (W + ox: the crop's second texel)
     int rb;           // canvas row of Q list index 0 (= y0 - 2)
     int Hn;           // rows kept in Q (= min(H + 4, N))
     int Hq;           // Hn rounded up to whole Q tiles (TK rows)
@@ -230,11 +235,14 @@ __device__ __forceinline__ float2 chroma_iq(typename Pix<FMT>::raw_t u)
 // =========================================================================
 // K1: luma rows -> half spectra of row pairs
 // =========================================================================
-template <int LOG2N, int FMT>
+// GEN (odd W or H): the composite taps of a pixel span i-2 .. i+1 and are
+// read as unmerged Tap4 entries (colT / rowT) instead of the 3-tap tables.
+template <int LOG2N, int FMT, bool GEN = false>
 __global__ __launch_bounds__(k1_threads<LOG2N>())
 void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pairs_per_frame,
                 int total_pairs, Geo g, const float4 *__restrict__ colW3,
-                const float4 *__restrict__ rowW3, const c2 *__restrict__ tw,
+                const float4 *__restrict__ rowW3, const Tap4 *__restrict__ colT,
+                const Tap4 *__restrict__ rowT, const c2 *__restrict__ tw,
                 c2 *__restrict__ G, size_t g_stride)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k1_groups<LOG2N>();
@@ -260,8 +268,32 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     // RGBA8: all 32 pixel loads of the thread in one batch; RGBA32F (4x the
     // registers): two batches of 16
     constexpr int UB = FMT == 0 ? 8 : 4;
-    if (valid) {
-        const float4 wa = rowW3[ra], wb = rowW3[ra + 1];
+    if constexpr (GEN) {
+        if (valid) {
+            const Tap4 ta = rowT[ra];
+            Tap4 tb = ra + 1 < g.H ? rowT[ra + 1] : ta;
+            if (ra + 1 >= g.H)
+                for (int m = 0; m < 4; ++m) tb.w[m] = 0.0f;   // the zero row of odd H
+            unsigned pa[4], pb[4];   // source row byte offsets
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                pa[m] = (unsigned)(wrap_near(ta.idx[m], g.H, g.edge) * g.W * BPP);
+                pb[m] = (unsigned)(wrap_near(tb.idx[m], g.H, g.edge) * g.W * BPP);
+            }
+            for (int i = t; i < g.W; i += T) {
+                float va = 0.0f, vb = 0.0f;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    va += ta.w[m] * luma_raw<FMT>(ld_off<raw_t>(img, pa[m] + (unsigned)i * BPP));
+                    vb += tb.w[m] * luma_raw<FMT>(ld_off<raw_t>(img, pb[m] + (unsigned)i * BPP));
+                }
+                V[i] = va;
+                V[g.W + i] = vb;
+            }
+        }
+    } else if (valid) {
+        // odd H: the last pair's second row is outside the image (zero)
+        const float4 wa = rowW3[ra], wb = ra + 1 < g.H ? rowW3[ra + 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const uint8_t *rowp[4];   // workgroup-uniform source row pointers
 #pragma unroll
         for (int d = 0; d < 4; ++d) rowp[d] = img + (unsigned)(wrap_near(ra - 1 + d, g.H, g.edge) * g.W * BPP);
@@ -296,11 +328,22 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         if (j == 4) __builtin_amdgcn_sched_barrier(0);     // two batches: bound VGPRs
         const int i = t + j * T - g.x0;                    // image column
         const int ic = min(max(i, 0), g.W - 1);
-        const float4 w = colW3[ic];   // weights of source columns i-1, i, i+1; .w: wrapped
-        const unsigned nb = __float_as_uint(w.w);          // (i-1) | (i+1) << 16
-        const int cl = nb & 0xffffu, cr = nb >> 16;
-        const float ya = w.x * V[cl] + w.y * V[ic] + w.z * V[cr];
-        const float yb = w.x * V[g.W + cl] + w.y * V[g.W + ic] + w.z * V[g.W + cr];
+        float ya = 0.0f, yb = 0.0f;
+        if constexpr (GEN) {
+            const Tap4 tc = colT[ic];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int c = wrap_near(tc.idx[m], g.W, g.edge);
+                ya += tc.w[m] * V[c];
+                yb += tc.w[m] * V[g.W + c];
+            }
+        } else {
+            const float4 w = colW3[ic];   // weights of source columns i-1, i, i+1; .w: wrapped
+            const unsigned nb = __float_as_uint(w.w);          // (i-1) | (i+1) << 16
+            const int cl = nb & 0xffffu, cr = nb >> 16;
+            ya = w.x * V[cl] + w.y * V[ic] + w.z * V[cr];
+            yb = w.x * V[g.W + cl] + w.y * V[g.W + ic] + w.z * V[g.W + cr];
+        }
         const bool in = valid && i >= 0 && i < g.W;
         v[j] = in ? mk(ya, yb) : mk(0.0f, 0.0f);
     }
@@ -335,8 +378,8 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         if (!valid) return;
         c2 *Gf = G + (size_t)frame * g_stride;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) st_off<float4>(Gf, (unsigned)((t + j * T) * g.H + ra) * 8u, o[j]);
-        if (t == 0) st_off<float4>(Gf, (unsigned)((N / 2) * g.H + ra) * 8u, o[4]);
+        for (int j = 0; j < 4; ++j) st_off<float4>(Gf, (unsigned)((t + j * T) * g.Hg + ra) * 8u, o[j]);
+        if (t == 0) st_off<float4>(Gf, (unsigned)((N / 2) * g.Hg + ra) * 8u, o[4]);
         return;
     }
     __syncthreads();   // split reads done before the staging overwrites the buffers
@@ -350,7 +393,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     c2 *Gf = G + (size_t)fr0 * g_stride;
     for (int e = threadIdx.x; e < (N / 2 + 1) * GPW; e += GPW * T) {
         const int f = e / GPW, c = e - f * GPW;
-        st_off<float4>(Gf, (unsigned)(f * g.H + ra0 + 2 * c) * 8u, stg[e]);
+        st_off<float4>(Gf, (unsigned)(f * g.Hg + ra0 + 2 * c) * 8u, stg[e]);
     }
 }
 
@@ -743,7 +786,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int rr = t + j * T - g.y0;
-            const unsigned off = rr >= 0 && rr < g.H ? (unsigned)(f * g.H + rr) * 8u : 0x80000000u;
+            const unsigned off = rr >= 0 && rr < g.H ? (unsigned)(f * g.Hg + rr) * 8u : 0x80000000u;
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
             const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, off, 0, 0);
             ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
@@ -752,7 +795,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int rr = t + j * T - g.y0;
-                const unsigned off = rr >= 0 && rr < g.H ? (unsigned)((N / 2) * g.H + rr) * 8u : 0x80000000u;
+                const unsigned off = rr >= 0 && rr < g.H ? (unsigned)((N / 2) * g.Hg + rr) * 8u : 0x80000000u;
                 gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, off, 0, 0));
             }
         }
@@ -1117,11 +1160,11 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
     }
     __syncthreads();
     if (!valid) return;
-    float *out = Yh + (size_t)frame * yh_stride + (size_t)ka * g.W;
-    if (g.x0 >= 4 && g.x0 % 4 == 0 && g.W % 4 == 0 && g.x0 + g.W + 4 <= N) {
+    float *out = Yh + (size_t)frame * yh_stride + (size_t)ka * g.Wy;
+    if (g.x0 >= 4 && g.x0 % 4 == 0 && g.Wy % 4 == 0 && g.x0 + g.Wy + 4 <= N) {
         // four outputs per thread from three aligned ds_read_b128 (taps c-2..c+5),
         // one 16-B store; same expression and order as the scalar form below
-        const int W4 = g.W / 4;
+        const int W4 = g.Wy / 4;
         for (int e = t; e < 2 * W4; e += T) {
             const int r = e >= W4 ? 1 : 0, X = 4 * (e - r * W4);
             const float4 *rw = reinterpret_cast<const float4 *>(raw + r * N + g.x0 + X);
@@ -1131,13 +1174,14 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
             o.y = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
             o.z = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
             o.w = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
-            *reinterpret_cast<float4 *>(out + (size_t)r * g.W + X) = o;
+            *reinterpret_cast<float4 *>(out + (size_t)r * g.Wy + X) = o;
         }
         return;
     }
-    const bool interior = g.x0 >= 2 && g.x0 + g.W + 2 <= N;
-    for (int e = t; e < 2 * g.W; e += T) {
-        const int r = e >= g.W ? 1 : 0, X = e - r * g.W;
+    // Wy = W columns (W + 1 for odd W: the crop's second texel)
+    const bool interior = g.x0 >= 2 && g.x0 + g.Wy + 2 <= N;
+    for (int e = t; e < 2 * g.Wy; e += T) {
+        const int r = e >= g.Wy ? 1 : 0, X = e - r * g.Wy;
         const float *rw = raw + r * N;
         const int c = g.x0 + X;
         float acc;
@@ -1148,7 +1192,7 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
             acc += bw.w1 * (rw[wrap_idx(c - 1, N, g.edge)] + rw[wrap_idx(c + 1, N, g.edge)]);
             acc += bw.w2 * (rw[wrap_idx(c - 2, N, g.edge)] + rw[wrap_idx(c + 2, N, g.edge)]);
         }
-        out[(size_t)r * g.W + X] = acc;
+        out[(size_t)r * g.Wy + X] = acc;
     }
 }
 
@@ -1218,7 +1262,7 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
     for (int v = 0; v < TR + 4; ++v) {   // unconditional loads at clamped addresses
         const int cy = wrap_near(g.y0 + i0 - 2 + v, g.N, g.edge);
         const int k = (cy - g.rb + 2 * g.N) & (g.N - 1);
-        const float y = ld_off<float>(Yf, (unsigned)(min(k, g.Hn - 1) * g.W + Xc) * 4u);
+        const float y = ld_off<float>(Yf, (unsigned)(min(k, g.Hn - 1) * g.Wy + Xc) * 4u);
         yv[v] = k < g.Hn ? y : 0.0f;
     }
     // halo columns j = TC, TC + 1 of the TR + 2 rows: one entry for each of
@@ -1259,6 +1303,66 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
     }
 }
 
+// K4 for odd W and/or H: the quad's edge then sits half a texel off the
+// texel grid (x0 + 0.5), and CropTexture (.cs:386-410) samples the final
+// texture between two texels (four when both are odd) with weights 1/2: output
+// pixel (X, Y) = mean of saturate(YIQ->RGB) at canvas texels x0 + X (+1),
+// y0 + Y (+1) (oracle mm_ref.c crop).  A texel outside the quad has I = Q = 0
+// (the cleared canvas) and the blurred Y' of that position.  One thread per
+// output pixel; the I/Q of a texel is the composite resample from the unmerged
+// Tap4 tables (taps on i-2 .. i+1 for odd sizes).
+template <int FMT>
+__global__ __launch_bounds__(256)
+void k_compose_odd(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__restrict__ frames_in,
+                   uint8_t *__restrict__ frames_out, size_t frame_bytes, int frame0, int nframes, Geo g,
+                   Blur5 bw, const Tap4 *__restrict__ colT, const Tap4 *__restrict__ rowT)
+{
+    const size_t npx = (size_t)g.W * g.H;
+    const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (e >= npx * nframes) return;
+    const int k = (int)(e / npx);
+    const int p = (int)(e - (size_t)k * npx);
+    const int Y = p / g.W, X = p - Y * g.W;
+    const int frame = frame0 + k;
+    const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
+    const float *Yf = Yh + (size_t)frame * yh_stride;
+    const float wt = (g.ox ? 0.5f : 1.0f) * (g.oy ? 0.5f : 1.0f);
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    for (int dy = 0; dy <= g.oy; ++dy)
+        for (int dx = 0; dx <= g.ox; ++dx) {
+            const int tx = X + dx, ty = Y + dy;   // texel's image column / row (may be W / H)
+            // Y': vertical 5-tap blur of Yh (list row of canvas row y0+ty+d is ty+2+d)
+            float yv[5];
+            for (int d = 0; d < 5; ++d) {
+                const int cy = wrap_near(g.y0 + ty - 2 + d, g.N, g.edge);
+                const int kk = (cy - g.rb + 2 * g.N) & (g.N - 1);
+                yv[d] = kk < g.Hn ? Yf[(size_t)kk * g.Wy + tx] : 0.0f;
+            }
+            const float yb = bw.w0 * yv[2] + bw.w1 * (yv[1] + yv[3]) + bw.w2 * (yv[0] + yv[4]);
+            float ci = 0.0f, cq = 0.0f;
+            if (tx < g.W && ty < g.H) {
+                const Tap4 tc = colT[tx], tr = rowT[ty];
+                for (int a = 0; a < 4; ++a) {
+                    if (tr.w[a] == 0.0f) continue;
+                    const int sr = wrap_near(tr.idx[a], g.H, g.edge);
+                    float hi = 0.0f, hq = 0.0f;
+                    for (int b = 0; b < 4; ++b) {
+                        const int sc = wrap_near(tc.idx[b], g.W, g.edge);
+                        const float2 iq = chroma_iq<FMT>(Pix<FMT>::raw(img, (size_t)sr * g.W + sc));
+                        hi += tc.w[b] * iq.x;
+                        hq += tc.w[b] * iq.y;
+                    }
+                    ci += tr.w[a] * hi;
+                    cq += tr.w[a] * hq;
+                }
+            }
+            acc[0] += wt * sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
+            acc[1] += wt * sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
+            acc[2] += wt * sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
+        }
+    Pix<FMT>::store(frames_out + (size_t)frame * frame_bytes, (unsigned)p, acc[0], acc[1], acc[2]);
+}
+
 // =========================================================================
 // f3 debug views: ProcessDebugView (.cs:234-257)
 // =========================================================================
@@ -1287,7 +1391,7 @@ void k_dbg_cols(const c2 *__restrict__ G, size_t g_stride, float *__restrict__ t
     const int kx = blockIdx.x % N, fr = frame0 + blockIdx.x / N;
     const int f = (kx + N / 2) & (N - 1);
     const bool mirror = f > N / 2;
-    const c2 *Gc = G + (size_t)fr * g_stride + (size_t)(mirror ? N - f : f) * g.H;
+    const c2 *Gc = G + (size_t)fr * g_stride + (size_t)(mirror ? N - f : f) * g.Hg;
     const float sgn = grp ? -1.0f : 1.0f;                     // (-1)^r
     c2 v[8];
 #pragma unroll

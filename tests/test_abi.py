@@ -38,7 +38,8 @@ def test_create_rejects_bad_arguments_without_gpu():
     p = mm355.Params.make()
     h = ctypes.c_void_p()
     L = mm355.lib()
-    assert L.mm_create(63, 48, ctypes.byref(p), 0, ctypes.byref(h)) == -2   # odd width
+    st = mm355.Params.make(mode=mm355.MODE_STEERABLE, orientations=8)
+    assert L.mm_create(63, 48, ctypes.byref(st), 0, ctypes.byref(h)) == -2  # odd width: steerable only
     assert L.mm_create(8192, 48, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N > 4096
     bad = mm355.Params.make()
     bad.orientations = 8
@@ -58,7 +59,7 @@ def test_create_fails_loudly_without_device():
 
 
 @pytest.mark.parametrize("W,H,edge", [(64, 48, 0), (64, 48, 1), (1920, 1080, 0), (200, 120, 1),
-                                      (256, 256, 0)])
+                                      (256, 256, 0), (63, 47, 0), (65, 49, 1), (1919, 1079, 0)])
 def test_resample_table_matches_oracle_pad(W, H, edge):
     """The composite (stretch x pad x Hann) taps reproduce the oracle's literal
     two-step bilinear pad of a separable test image."""

@@ -393,3 +393,44 @@ def test_bench_sharded_ring_equals_single_rank():
                "--warmup", "1"])
     assert one["frames"] == two["frames"] == [0, 47]
     assert one["checksums"] == two["checksums"]
+
+
+# ---- odd frame sizes (the reference takes any Screen.width/height, .cs:298-302) ----
+# N - W odd puts the PadTexture quad half a texel off the grid (.cs:358-381) and
+# makes CropTexture sample between two texels; the oracle restates both.
+@pytest.mark.parametrize("W,H,L,S,edge,mode", [
+    (63, 47, 5, 10.0, 0, "frame"), (63, 48, 5, 25.0, 1, "stream"), (64, 47, 4, 25.0, 0, "frame"),
+    (65, 49, 5, 9.7, 0, "stream"), (201, 121, 5, 25.0, 0, "stream"), (33, 17, 3, 10.0, 1, "frame")])
+def test_odd_sizes_f32(W, H, L, S, edge, mode):
+    fr = T.synth(W, H, 5)
+    ref = T.oracle_run(W, H, fr, L, S, edge)
+    got = T.gpu_run(W, H, fr, L, S, edge, mode=mode, batch=3)
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r, integer_scale=float(S).is_integer())
+        assert np.all(g[..., 3] == 1.0)
+
+
+def test_odd_size_standard_mode_and_u8():
+    W, H = 97, 63
+    fr = T.synth(W, H, 4)
+    std = dict(apply=True, low=0.05, high=0.4, steep=3.0, sens=1.5, edge=0.8)
+    ref = T.oracle_run(W, H, fr, 5, 25.0, standard=std)
+    got = T.gpu_run(W, H, fr, 5, 25.0, standard=std)
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r)
+    fr8 = T.synth(W, H, 4, fmt="u8")
+    ref8 = T.oracle_run(W, H, fr8, 5, 25.0)
+    got8 = T.gpu_run(W, H, fr8, 5, 25.0, mode="stream")
+    assert np.array_equal(got8[0], fr8[0])
+    T.assert_close_u8(np.stack(got8[1:]), np.stack(ref8[1:]))
+
+
+def test_odd_1919x1079_u8_stream():
+    """1080p minus one pixel each way (N = 2048, both offsets fractional)."""
+    W, H = 1919, 1079
+    fr = T.synth(W, H, 3, fmt="u8")
+    ref = T.oracle_run(W, H, fr, 5, 25.0)
+    got = T.gpu_run(W, H, fr, 5, 25.0, mode="stream")
+    assert np.array_equal(got[0], fr[0])
+    T.assert_close_u8(np.stack(got[1:]), np.stack(ref[1:]))
