@@ -495,7 +495,7 @@ def main():
                               "profiles/r02_valu_calib.json) / (1024 SIMDs x kernel cycles)"}
         except Exception:
             valu = None
-    B = survey_bytes_per_frame(W, H, N)
+    B_survey = survey_bytes_per_frame(W, H, N)
     batch = B
 
     result = {
@@ -526,8 +526,8 @@ def main():
                                     "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch",
                      "compute": valu},
         "frame_roofline": (frame_roofline(W, H, N, fps / world, batch) if not steer else None),
-        "survey_model": {"bytes_per_frame": B,
-                         "equivalent_GBps_per_gpu": round(B * fps / world / 1e9, 1),
+        "survey_model": {"bytes_per_frame": B_survey,
+                         "equivalent_GBps_per_gpu": round(B_survey * fps / world / 1e9, 1),
                          "note": "SURVEY.md §8(d) B=W*H*(2b_in+b_out)+6*N^2*8 charges dense "
                                  "N x N hand-offs and a per-frame state round trip that this "
                                  "design does not move; B x fps is an equivalent rate, not a "

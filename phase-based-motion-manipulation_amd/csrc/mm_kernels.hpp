@@ -411,8 +411,13 @@ __device__ __forceinline__ float smooth01(float x)   // HLSL smoothstep(0,1,x)
 __device__ __forceinline__ float fast_atan2(float y, float x)
 {
     const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    // max3 with the smallest normal float: atan2(0, 0) = 0 without a select
+    // (0 * rcp(2^-126) = 0); no nonzero argument of the ops is that small
+    // (mn by the octant compare, not fminf: its NaN canonicalisation costs two
+    // more instructions on operands the compiler cannot prove canonical)
+    const bool steep = ay > ax;
+    const float mx = fmaxf(fmaxf(ax, ay), 1.17549435e-38f), mn = steep ? ax : ay;
+    const float a = mn * __builtin_amdgcn_rcpf(mx);
     const float s = a * a;
     float r = -0.00405455008149147f;
     r = r * s + 0.021862903609871864f;
@@ -423,7 +428,7 @@ __device__ __forceinline__ float fast_atan2(float y, float x)
     r = r * s - 0.33329859375953674f;
     r = r * s + 0.9999993443489075f;
     r *= a;
-    if (ay > ax) r = 1.57079632679489662f - r;
+    if (steep) r = 1.57079632679489662f - r;
     if (x < 0.0f) r = 3.14159265358979324f - r;
     return copysignf(r, y);
 }
@@ -505,10 +510,11 @@ __device__ __forceinline__ c2 spectral_op(c2 c, c2 p, int fx, int fy, const Spec
 // what depends only on (fx, fy) is evaluated once per launch into LDS (N/2+1
 // entries: every mask is symmetric in fy) instead of once per bin and frame.
 //   MM_K2_PYR_TAB (pyramid): x = m_a, the first middle-band mask nonzero at
-//     the bin; y = -(hp + lp), the always-passed levels 0 and L-1, when at most
-//     one band is nonzero (sign bit set, -0.0 included), else y = m_b, the
-//     second band, and hp + lp is evaluated inline (a divergent branch that
-//     only waves holding such bins take; none for L <= 5 at default bands).
+//     the bin; y = -(m_a + hp + lp), minus the bin's mask sum (hp, lp: the
+//     always-passed levels 0 and L-1), when at most one band is nonzero (sign
+//     bit set, -0.0 included), else y = m_b, the second band, and hp + lp is
+//     evaluated inline (a divergent branch that only waves holding such bins
+//     take; none for L <= 5 at default bands).
 //     The host checks that no 3 bands overlap.
 //   MM_MODE_STANDARD: (w, 0), w = calculate_bandpass_weight (:74-122).
 constexpr int MM_K2_PYR_TAB = 2;
@@ -546,7 +552,9 @@ __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
                 }
             }
         }
-        return make_float2(ma, mb != 0.0f ? mb : -mfix);
+        // one band: y = -(m_a + hp + lp), the bin's whole mask sum (sign bit set,
+        // -0.0 included); two bands: y = m_b > 0
+        return make_float2(ma, mb != 0.0f ? mb : -(ma + mfix));
     }
 }
 
@@ -582,7 +590,7 @@ __device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spe
     const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
     float mpass, mb;
     if (__builtin_signbit(mt.y)) {   // static hp + lp from the table
-        mpass = -mt.y;
+        mpass = -mt.y - mt.x;
         mb = 0.0f;
     } else {                         // two bands at this bin: hp + lp inline
         const float ux = (float)fx * (1.0f / (float)N);
@@ -610,19 +618,22 @@ __device__ __forceinline__ c2 pyramid_op_t(c2 c, c2 p, int fx, int fy, const Spe
 
 // pyramid_op_t for a bin with at most one middle band (table entry y < 0,
 // the usual case: bands touch only where their masks are 0), without
-// branches: the gated-in phase factor is computed for every bin and selected
-// at the end, so the compiler can interleave several bins' dependency chains
-// (atan2 polynomial, v_sin/v_cos) instead of running them one after another.
+// branches or selects on the phase factor, so that the compiler interleaves
+// several bins' dependency chains (atan2 polynomial, v_sin/v_cos) instead of
+// branching around each one under an exec mask:
+//   w = mpass + mmag e^{i S delta},  mmag = gated ? 0 : m_a,  mpass = sum - mmag
+// (mmag = 0 gives w = (mpass, 0) exactly: cos/sin are finite for every
+// argument, fast_atan2(0, 0) = 0).  u = p conj c and c w use the packed
+// multiplies (their operands are plain VALU results, never a transcendental's).
 __device__ __forceinline__ c2 pyramid_op_1band(c2 c, c2 p, const Spec &sp, float2 mt)
 {
     const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
-    const bool gate = mt.x * mt.x * mn2 < sp.tau2_nn;
-    const float mpass = gate ? mt.x - mt.y : -mt.y;
-    const float mmag = gate ? 0.0f : mt.x;
-    const float rev = fast_atan2(p.y * c.x - p.x * c.y, p.x * c.x + p.y * c.y) * sp.S_rev;
+    const float mmag = mt.x * mt.x * mn2 < sp.tau2_nn ? 0.0f : mt.x;
+    const float mpass = -mt.y - mmag;
+    const c2 u = mul_conj(p, c);
+    const float rev = fast_atan2(u.y, u.x) * sp.S_rev;
     const float cw = __builtin_amdgcn_cosf(rev), sw = __builtin_amdgcn_sinf(rev);
-    const c2 w = mmag > 0.0f ? mk(mmag * cw + mpass, mmag * sw) : mk(mpass, 0.0f);
-    return mul_c(c, w);
+    return mul(c, mk(mmag * cw + mpass, mmag * sw));
 }
 
 template <int MODE>
@@ -903,11 +914,15 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
                 // no bin of this wave has two middle bands: branch-free op, bins
                 // interleaved MM_K2_OPG at a time
+                // bin j: fy = fft_bin(t, 0) + j N/8, table entry fy for j < 4,
+                // N - fy for j >= 4 (fy <= N/2 exactly for j < 4)
+                const int fy0 = fft_bin<LOG2N>(t, 0);
+                const float2 *tlo = tab0 + fy0, *thi = tab0 - fy0;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
-                    const int fy = fft_bin<LOG2N>(t, j);
-                    const c2 a = pyramid_op_1band(v[j], prev[j], sp, tab0[fy <= N / 2 ? fy : N - fy]);
+                    const float2 mt = j < 4 ? tlo[j * (N / 8)] : thi[N - j * (N / 8)];
+                    const c2 a = pyramid_op_1band(v[j], prev[j], sp, mt);
                     prev[j] = v[j];
                     v[j] = a;
                 }

@@ -434,3 +434,4 @@ def test_odd_1919x1079_u8_stream():
     got = T.gpu_run(W, H, fr, 5, 25.0, mode="stream")
     assert np.array_equal(got[0], fr[0])
     T.assert_close_u8(np.stack(got[1:]), np.stack(ref[1:]))
+
