@@ -673,7 +673,7 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 {
     return (size_t)k2_groups<LOG2N>() *
                (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_entries<LOG2N>()) +
-           sizeof(float2) * k2_tab_entries<LOG2N>() + sizeof(c2) * 2 + sizeof(float) * (1 << LOG2N);
+           sizeof(float2) * k2_tab_entries<LOG2N>() + sizeof(c2) * 4 + sizeof(float) * (1 << LOG2N);
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
@@ -684,9 +684,9 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 // packed group unpacks F0, FN from Z(fy), Z(N-fy) (partner bins through LDS)
 // and runs the same number of ops per thread as any other group: a thread's
 // bins fy < N/2 (j < 4) carry column 0's op at fy, its bins fy > N/2 carry
-// column N/2's op at N - fy, and thread 0 alone adds the two real bins of
-// column N/2 (0 and N/2).  Its F_{t-1} registers hold those same bins (FN(0),
-// FN(N/2) in ldsX).  A second exchange recombines A = A0 + i AN per bin.
+// column N/2's op at N - fy; the two real bins of column N/2 (0 and N/2) are
+// one extra op each for threads T/4 and 3T/4 (F_{t-1} and the result in ldsX).
+// A second exchange recombines A = A0 + i AN per bin.
 // (The packed block is the kernel's critical path: every block is resident at
 // once, so its extra work is the kernel's.)
 #ifndef MM_K2_OPG
@@ -729,7 +729,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     // group), and one frame's Q values by list row (staged like the others: no
     // global round trip and no store the next frame's loads must wait for)
     c2 *ldsX = reinterpret_cast<c2 *>(tabN + TE);
-    float *stgN = reinterpret_cast<float *>(ldsX + 2);
+    float *stgN = reinterpret_cast<float *>(ldsX + 4);
     const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
@@ -775,7 +775,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         const size_t at = packed && !pk_col0(j, fy) ? (size_t)(N / 2) * N + (N - fy) : (size_t)f * N + fy;
         prev[j] = state_in ? state_in[at] : mk(0.0f, 0.0f);
     }
-    if (packed && t0 == 0) {   // FN(0), FN(N/2): thread 0's alone, no barrier
+    if (packed && t0 == 0) {   // FN(0), FN(N/2) of F_{t-1} (read after the loop's barriers)
         ldsX[0] = state_in ? state_in[(size_t)(N / 2) * N] : mk(0.0f, 0.0f);
         ldsX[1] = state_in ? state_in[(size_t)(N / 2) * N + N / 2] : mk(0.0f, 0.0f);
     }
@@ -844,7 +844,10 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         // times 917 vs 1357 us per 100 frames).  Alternating the priority
         // every frame between the first-dispatched half of the grid and the
         // second keeps a pair in step (1082..1305 us).
-        if ((fr ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
+        // Block 0 (the packed group's extra exchanges: the kernel's critical
+        // path, phase stamps) keeps the highest priority throughout.
+        if (blk0) __builtin_amdgcn_s_setprio(3);
+        else if ((fr ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
         load_g(fr < nframes ? fr : nframes - 1, t);
         K2_STAMP(0);
@@ -949,10 +952,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             }
             __syncthreads();
             // v[j] becomes A0(fy) (j < 4) / AN(N - fy) (j >= 4)
-            c2 an0 = mk(0.0f, 0.0f), anh = mk(0.0f, 0.0f);   // thread 0: AN(0), AN(N/2)
             if (packed) {
                 // unpack every bin (partner Z(N - fy) from LDS), then the ops
-                c2 fn0 = mk(0.0f, 0.0f), fnh = mk(0.0f, 0.0f);   // thread 0: FN(0), FN(N/2)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int fy = fft_bin<LOG2N>(t, j);
@@ -960,8 +961,6 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                     const c2 f0 = mk(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));    // F0(fy)
                     const c2 fn = mk(0.5f * (z.y + m.y), -0.5f * (z.x - m.x));   // FN(fy)
                     v[j] = pk_col0(j, fy) ? f0 : mk(fn.x, -fn.y);                // or FN(N - fy)
-                    if (j == 0) fn0 = fn;
-                    if (j == 4) fnh = fn;
                 }
                 if (!pass_frame) {
                     if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
@@ -985,17 +984,24 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                         }
                     }
                     __builtin_amdgcn_sched_barrier(0);
-                    if (t == 0) {   // column N/2's real bins 0 and N/2
-                        an0 = k2_op<LOG2N, MODE>(fn0, ldsX[0], N / 2, 0, sp, tabN);
-                        anh = k2_op<LOG2N, MODE>(fnh, ldsX[1], N / 2, N / 2, sp, tabN);
-                    }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) prev[j] = v[j];
                 }
-                if (t == 0) {
-                    ldsX[0] = fn0;
-                    ldsX[1] = fnh;
+                // column N/2's real bins 0 and N/2: FN = Im Z there (Z(0) and
+                // Z(N/2) are their own partners, still in LDS), op against
+                // F_{t-1} in ldsX[0..1]; AN to ldsX[2..3] for thread 0's
+                // recombine.  Threads T/4 and 3T/4 (waves 1 and 3 at N = 2048,
+                // not wave 0, which holds fy = 0 and N/2 in the recombine).
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    if (t == (x ? 3 * T / 4 : T / 4)) {
+                        const int fyx = x ? N / 2 : 0;
+                        const c2 z = lds[pad8(fyx)];
+                        const c2 fn = mk(0.5f * (z.y + z.y), -0.5f * (z.x - z.x));
+                        if (!pass_frame) ldsX[2 + x] = k2_op<LOG2N, MODE>(fn, ldsX[x], N / 2, fyx, sp, tabN);
+                        ldsX[x] = fn;
+                    }
                 }
             } else {
                 regular_op();   // the block's other group, between the same barriers
@@ -1019,7 +1025,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                     c2 a0, an;
                     if (pk_col0(j, fy)) {   // A(fy) = A0(fy) + i AN(fy)
                         a0 = v[j];
-                        an = fy == 0 ? an0 : (fy == N / 2 ? anh : lds[LN + fy]);
+                        an = fy == 0 ? ldsX[2] : (fy == N / 2 ? ldsX[3] : lds[LN + fy]);
                     } else {                // A(fy) = conj A0(N-fy) + i conj AN(N-fy)
                         const c2 b = lds[pad8(N - fy)];
                         a0 = mk(b.x, -b.y);
