@@ -337,6 +337,31 @@ __device__ __forceinline__ int fft_bin(int t, int j)
     else return (t >> 6) + C * ((t & 63) + 64 * j);
 }
 
+// LDS slot of bin f in a bin-indexed exchange after fft_dif (all N bins):
+// bins f = w (mod C) contiguous, residue regions N/C + 8 apart.  fft_dif's
+// layout writes (lane l of wave w: bins w + C (l + 64 j)) land on consecutive
+// slots, and natural-order reads of 32 lanes (f = c + l, c = 0 mod C) spread
+// the C residues 16 banks apart: both conflict-free on gfx950 (pad8 on f:
+// 2-way writes and reads; tools/lds_banks.py).  N + 8 C slots (<= lds_complex).
+template <int LOG2N>
+__host__ __device__ constexpr int zslot(int f)
+{
+    constexpr int C = fft_c_v(LOG2N), N = 1 << LOG2N;
+    return C == 1 ? f : (f % C) * (N / C + 8) + f / C;
+}
+// The same for entries e = 0..N/2 (half spectra): regions N/(2C) + 8 apart,
+// C (N/(2C) + 8) slots
+template <int LOG2N>
+__host__ __device__ constexpr int zslot_h(int e)
+{
+    constexpr int C = fft_c_v(LOG2N), N = 1 << LOG2N;
+    return C == 1 ? e : (e % C) * (N / (2 * C) + 8) + e / C;
+}
+template <int LOG2N> constexpr int zslot_h_size()
+{
+    return fft_c_v(LOG2N) == 1 ? (1 << LOG2N) / 2 + 1 : (1 << LOG2N) / 2 + 8 * fft_c_v(LOG2N);
+}
+
 // Twiddle bases of fft_dif / fft_dit (forward direction): the inner passes'
 // (slots 4, 8, from the W_N table at stride C) and, for C > 1, the outer
 // stage's W_N^{n2} for the thread's H values n2 (slots 12 + h).

@@ -353,11 +353,11 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     fft_dif<LOG2N, -1>(v, t, lds, wb);
     __syncthreads();   // every wave done with its LDS region
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lds[pad8(fft_bin<LOG2N>(t, j))] = v[j];
+    for (int j = 0; j < 8; ++j) lds[zslot<LOG2N>(fft_bin<LOG2N>(t, j))] = v[j];
     __syncthreads();
     // half spectra of rows (ra, ra+1) at bins f = t + jT (j < 4) and N/2 (j = 4)
     auto split = [&](int f) {
-        c2 zf = lds[pad8(f)], zm = lds[pad8((N - f) & (N - 1))];
+        c2 zf = lds[zslot<LOG2N>(f)], zm = lds[zslot<LOG2N>((N - f) & (N - 1))];
         // Y_a = (Z[f] + conj Z[N-f]) / 2 ;  Y_b = (Z[f] - conj Z[N-f]) / 2i
         float4 o;
         o.x = 0.5f * (zf.x + zm.x);
@@ -383,17 +383,23 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         return;
     }
     __syncthreads();   // split reads done before the staging overwrites the buffers
-    float4 *stg = reinterpret_cast<float4 *>(lds_all);   // [N/2 + 1][GPW]
+    // [GPW][SS] (group-major, SS = N/2+1 rounded up to 8 mod 16 float4: the two
+    // groups' entries of a bin 32 banks apart) when GPW == 2; [N/2 + 1][GPW]
+    // otherwise (small N: many groups, no room for padding)
+    float4 *stg = reinterpret_cast<float4 *>(lds_all);
+    constexpr int SS = (N / 2 + 1 + 7) / 16 * 16 + 8;
+    constexpr bool GM = GPW == 2 && 2 * SS * 2 <= 2 * lds_complex<N>();
+    auto sidx = [&](int f, int c) { return GM ? c * SS + f : f * GPW + c; };
 #pragma unroll
-    for (int j = 0; j < 4; ++j) stg[(t + j * T) * GPW + grp] = o[j];
-    if (t == 0) stg[(N / 2) * GPW + grp] = o[4];
+    for (int j = 0; j < 4; ++j) stg[sidx(t + j * T, grp)] = o[j];
+    if (t == 0) stg[sidx(N / 2, grp)] = o[4];
     __syncthreads();
     if (lblk >= total_pairs) return;   // whole block past the end (total % GPW == 0)
     const int fr0 = lblk / pairs_per_frame, ra0 = 2 * (lblk % pairs_per_frame);
     c2 *Gf = G + (size_t)fr0 * g_stride;
     for (int e = threadIdx.x; e < (N / 2 + 1) * GPW; e += GPW * T) {
         const int f = e / GPW, c = e - f * GPW;
-        st_off<float4>(Gf, (unsigned)(f * g.Hg + ra0 + 2 * c) * 8u, stg[e]);
+        st_off<float4>(Gf, (unsigned)(f * g.Hg + ra0 + 2 * c) * 8u, stg[sidx(f, c)]);
     }
 }
 
@@ -646,6 +652,21 @@ __device__ __forceinline__ c2 standard_op_t(c2 c, c2 p, const Spec &sp, float2 m
     return scale(mul_c(c, mk(__cosf(ph), __sinf(ph))), sp.inv_nn);
 }
 
+template <int LOG2N> constexpr int k2_tab_entries() { return (1 << LOG2N) / 2 + 1; }
+// Per-bin table slot of entry e (0 <= e <= N/2): entries e = w (mod C) are
+// contiguous (slot (e mod C) Q + e / C, Q = ceil(entries / C)), so that a
+// wave's bins fy = w + C (l + 64 j) (fft_bin: one residue w per wave) read
+// consecutive slots, and the mirrored bins N - fy consecutive slots backwards:
+// no bank conflicts (natural order: lanes 8 C bytes apart, 4-way at C = 4).
+template <int LOG2N> constexpr int k2_tab_q() { return (k2_tab_entries<LOG2N>() + fft_c_v(LOG2N) - 1) / fft_c_v(LOG2N); }
+template <int LOG2N> constexpr int k2_tab_slots() { return k2_tab_q<LOG2N>() * fft_c_v(LOG2N); }
+template <int LOG2N>
+__host__ __device__ constexpr int k2_tix(int e)
+{
+    constexpr int C = fft_c_v(LOG2N);
+    return C == 1 ? e : (e % C) * k2_tab_q<LOG2N>() + e / C;
+}
+
 // MODE: MM_MODE_PYRAMID (dynamic masks), MM_MODE_STANDARD or MM_K2_PYR_TAB (tables)
 template <int LOG2N, int MODE>
 __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, const float2 *tab)
@@ -654,13 +675,12 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
     if constexpr (MODE == MM_MODE_PYRAMID) {
         return pyramid_op<LOG2N>(c, p, fx, fy, sp);
     } else {
-        const float2 mt = tab[fy <= N / 2 ? fy : N - fy];
+        const float2 mt = tab[k2_tix<LOG2N>(fy <= N / 2 ? fy : N - fy)];
         if constexpr (MODE == MM_MODE_STANDARD) return standard_op_t<MODE>(c, p, sp, mt);
         else return pyramid_op_t<LOG2N>(c, p, fx, fy, sp, mt);
     }
 }
 
-template <int LOG2N> constexpr int k2_tab_entries() { return (1 << LOG2N) / 2 + 1; }
 // k_cols runs at least two columns per workgroup, so that a Q row receives one
 // 16-B (or wider) piece per workgroup instead of one 8-B value per column
 template <int LOG2N> constexpr int k2_groups() { return groups_at_least<LOG2N, MM_K2_GROUPS>(); }
@@ -672,8 +692,8 @@ template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * ff
 template <int LOG2N> constexpr size_t k2_lds_bytes()
 {
     return (size_t)k2_groups<LOG2N>() *
-               (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_entries<LOG2N>()) +
-           sizeof(float2) * k2_tab_entries<LOG2N>() + sizeof(c2) * 4 + sizeof(float) * (1 << LOG2N);
+               (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_slots<LOG2N>()) +
+           sizeof(float2) * k2_tab_slots<LOG2N>() + sizeof(c2) * 4 + sizeof(float) * (1 << LOG2N);
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
@@ -717,18 +737,18 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                                             const c2 *__restrict__ tw, int blk)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
-    constexpr int TE = k2_tab_entries<LOG2N>();
+    constexpr int TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     // group index: wave-uniform (scalar) when a group spans whole waves
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
     const int t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
-    float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TE;
-    float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TE;
+    float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TS;
+    float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TS;
     // column N/2: F_{t-1} at its real bins 0 and N/2 (thread 0 of the packed
     // group), and one frame's Q values by list row (staged like the others: no
     // global round trip and no store the next frame's loads must wait for)
-    c2 *ldsX = reinterpret_cast<c2 *>(tabN + TE);
+    c2 *ldsX = reinterpret_cast<c2 *>(tabN + TS);
     float *stgN = reinterpret_cast<float *>(ldsX + 4);
     const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
@@ -742,10 +762,10 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             // pyramid table: masks pre-scaled by inv_nn (a power of two: exact)
             const float ks = MODE == MM_K2_PYR_TAB ? sp.inv_nn : 1.0f;
             const float2 b0 = bin_static<LOG2N, MODE>(f, e, sp);
-            tab0[e] = make_float2(b0.x * ks, b0.y * ks);
+            tab0[k2_tix<LOG2N>(e)] = make_float2(b0.x * ks, b0.y * ks);
             if (packed) {
                 const float2 bn = bin_static<LOG2N, MODE>(N / 2, e, sp);
-                tabN[e] = make_float2(bn.x * ks, bn.y * ks);
+                tabN[k2_tix<LOG2N>(e)] = make_float2(bn.x * ks, bn.y * ks);
             }
         }
         __syncthreads();
@@ -761,11 +781,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int fy = fft_bin<LOG2N>(t0, j);
-            if (packed && !pk_col0(j, fy)) two |= !__builtin_signbit(tabN[N - fy].y);
-            else two |= !__builtin_signbit(tab0[fy <= N / 2 ? fy : N - fy].y);
+            if (packed && !pk_col0(j, fy)) two |= !__builtin_signbit(tabN[k2_tix<LOG2N>(N - fy)].y);
+            else two |= !__builtin_signbit(tab0[k2_tix<LOG2N>(fy <= N / 2 ? fy : N - fy)].y);
         }
         if (packed && t0 == 0)
-            two |= !__builtin_signbit(tabN[0].y) || !__builtin_signbit(tabN[N / 2].y);
+            two |= !__builtin_signbit(tabN[k2_tix<LOG2N>(0)].y) || !__builtin_signbit(tabN[k2_tix<LOG2N>(N / 2)].y);
         wave_two_band = __any(two);
     }
     c2 prev[8];
@@ -917,14 +937,21 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
                 // no bin of this wave has two middle bands: branch-free op, bins
                 // interleaved MM_K2_OPG at a time
-                // bin j: fy = fft_bin(t, 0) + j N/8, table entry fy for j < 4,
-                // N - fy for j >= 4 (fy <= N/2 exactly for j < 4)
+                // bin j: fy = fy0 + j N/8 (fy0 = fft_bin(t, 0)), table entry fy
+                // for j < 4, N - fy for j >= 4 (fy <= N/2 exactly for j < 4).
+                // N/8 is a multiple of C, so both are slots of two per-frame
+                // bases plus immediates (k2_tix): entry fy0 + m C at slot
+                // k2_tix(fy0) + m, entry M - fy0 (M a multiple of C) at slot
+                // k2_tix(C - w) - 1 - fy0 / C + M / C for w = fy0 mod C > 0.
+                constexpr int C = fft_c_v(LOG2N);
                 const int fy0 = fft_bin<LOG2N>(t, 0);
-                const float2 *tlo = tab0 + fy0, *thi = tab0 - fy0;
+                const int w = fy0 % C;
+                const float2 *tlo = tab0 + k2_tix<LOG2N>(fy0);
+                const float2 *thi = tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
-                    const float2 mt = j < 4 ? tlo[j * (N / 8)] : thi[N - j * (N / 8)];
+                    const float2 mt = j < 4 ? tlo[j * (N / 8) / C] : thi[(N - j * (N / 8)) / C];
                     const c2 a = pyramid_op_1band(v[j], prev[j], sp, mt);
                     prev[j] = v[j];
                     v[j] = a;
@@ -948,7 +975,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             __syncthreads();
             if (packed) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) lds[pad8(fft_bin<LOG2N>(t, j))] = v[j];
+                for (int j = 0; j < 8; ++j) lds[zslot<LOG2N>(fft_bin<LOG2N>(t, j))] = v[j];
             }
             __syncthreads();
             // v[j] becomes A0(fy) (j < 4) / AN(N - fy) (j >= 4)
@@ -957,7 +984,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int fy = fft_bin<LOG2N>(t, j);
-                    const c2 z = v[j], m = lds[pad8((N - fy) & (N - 1))];
+                    const c2 z = v[j], m = lds[zslot<LOG2N>((N - fy) & (N - 1))];
                     const c2 f0 = mk(0.5f * (z.x + m.x), 0.5f * (z.y - m.y));    // F0(fy)
                     const c2 fn = mk(0.5f * (z.y + m.y), -0.5f * (z.x - m.x));   // FN(fy)
                     v[j] = pk_col0(j, fy) ? f0 : mk(fn.x, -fn.y);                // or FN(N - fy)
@@ -969,7 +996,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                             __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
                             const int fy = fft_bin<LOG2N>(t, j);
                             const c2 c = v[j];
-                            v[j] = pyramid_op_1band(c, prev[j], sp, pk_col0(j, fy) ? tab0[fy] : tabN[N - fy]);
+                            v[j] = pyramid_op_1band(c, prev[j], sp, pk_col0(j, fy) ? tab0[k2_tix<LOG2N>(fy)]
+                                                                                   : tabN[k2_tix<LOG2N>(N - fy)]);
                             prev[j] = c;
                         }
                     } else {
@@ -997,7 +1025,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                 for (int x = 0; x < 2; ++x) {
                     if (t == (x ? 3 * T / 4 : T / 4)) {
                         const int fyx = x ? N / 2 : 0;
-                        const c2 z = lds[pad8(fyx)];
+                        const c2 z = lds[zslot<LOG2N>(fyx)];
                         const c2 fn = mk(0.5f * (z.y + z.y), -0.5f * (z.x - z.x));
                         if (!pass_frame) ldsX[2 + x] = k2_op<LOG2N, MODE>(fn, ldsX[x], N / 2, fyx, sp, tabN);
                         ldsX[x] = fn;
@@ -1007,14 +1035,16 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                 regular_op();   // the block's other group, between the same barriers
             }
             __syncthreads();   // partner reads of Z done: the buffer takes the ops
-            // A0 at pad8(fy), AN at LN + fy (fy <= N/2)
-            constexpr int LN = lds_complex<N>() - (N / 2 + 1);
+            // A0 at zslot_h(fy), AN at ZH + zslot_h(fy) (fy <= N/2): each
+            // wave's writes and reads are consecutive slots (tools/lds_banks.py)
+            constexpr int ZH = zslot_h_size<LOG2N>();
+            static_assert(2 * ZH <= lds_complex<N>(), "recombine exchange fits the buffer");
             if (packed && !pass_frame) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int fy = fft_bin<LOG2N>(t, j);
-                    if (pk_col0(j, fy)) lds[pad8(fy)] = v[j];
-                    else lds[LN + N - fy] = v[j];
+                    if (pk_col0(j, fy)) lds[zslot_h<LOG2N>(fy)] = v[j];
+                    else lds[ZH + zslot_h<LOG2N>(N - fy)] = v[j];
                 }
             }
             __syncthreads();
@@ -1025,9 +1055,9 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                     c2 a0, an;
                     if (pk_col0(j, fy)) {   // A(fy) = A0(fy) + i AN(fy)
                         a0 = v[j];
-                        an = fy == 0 ? ldsX[2] : (fy == N / 2 ? ldsX[3] : lds[LN + fy]);
+                        an = fy == 0 ? ldsX[2] : (fy == N / 2 ? ldsX[3] : lds[ZH + zslot_h<LOG2N>(fy)]);
                     } else {                // A(fy) = conj A0(N-fy) + i conj AN(N-fy)
-                        const c2 b = lds[pad8(N - fy)];
+                        const c2 b = lds[zslot_h<LOG2N>(N - fy)];
                         a0 = mk(b.x, -b.y);
                         an = mk(v[j].x, -v[j].y);
                     }
