@@ -205,13 +205,17 @@ __device__ __forceinline__ float chroma_q(float4 c) { return 0.211f * c.x + -0.5
 __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
 
 // Y of a raw pixel (RGBA8: 1/255 folded into the RGBToYIQ row).
+// K1's luma in units of kLumaUnit<FMT>: RGBA8 as the exact integer
+// 299 R + 587 G + 114 B (two v_dot4_u32_u8: 299 = 256 + 43, 587 = 2 * 256 + 75,
+// and one convert; RGBToYIQ's 0.299/0.587/0.114 of R/255 ... times 255000),
+// whose unit 1/255000 folds into the resample weights; RGBA32F as luma().
+template <int FMT> constexpr float kLumaUnit = FMT == 0 ? 1.0f / 255000.0f : 1.0f;
 template <int FMT>
-__device__ __forceinline__ float luma_raw(typename Pix<FMT>::raw_t u)
+__device__ __forceinline__ float luma_units(typename Pix<FMT>::raw_t u)
 {
     if constexpr (FMT == 0) {
-        constexpr float k = 1.0f / 255.0f;
-        return (0.299f * k) * (float)(u & 255u) + (0.587f * k) * (float)((u >> 8) & 255u) +
-               (0.114f * k) * (float)((u >> 16) & 255u);
+        const unsigned hi = __builtin_amdgcn_udot4(u, 0x00000201u, 0u, false);    // R + 2 G
+        return (float)__builtin_amdgcn_udot4(u, 0x00724B2Bu, hi << 8, false);   // + 43 R + 75 G + 114 B
     } else {
         return luma(u);
     }
@@ -270,10 +274,13 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     constexpr int UB = FMT == 0 ? 8 : 4;
     if constexpr (GEN) {
         if (valid) {
-            const Tap4 ta = rowT[ra];
+            Tap4 ta = rowT[ra];
             Tap4 tb = ra + 1 < g.H ? rowT[ra + 1] : ta;
-            if (ra + 1 >= g.H)
-                for (int m = 0; m < 4; ++m) tb.w[m] = 0.0f;   // the zero row of odd H
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                ta.w[m] *= kLumaUnit<FMT>;
+                tb.w[m] = ra + 1 < g.H ? tb.w[m] * kLumaUnit<FMT> : 0.0f;   // the zero row of odd H
+            }
             unsigned pa[4], pb[4];   // source row byte offsets
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -284,8 +291,8 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
                 float va = 0.0f, vb = 0.0f;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    va += ta.w[m] * luma_raw<FMT>(ld_off<raw_t>(img, pa[m] + (unsigned)i * BPP));
-                    vb += tb.w[m] * luma_raw<FMT>(ld_off<raw_t>(img, pb[m] + (unsigned)i * BPP));
+                    va += ta.w[m] * luma_units<FMT>(ld_off<raw_t>(img, pa[m] + (unsigned)i * BPP));
+                    vb += tb.w[m] * luma_units<FMT>(ld_off<raw_t>(img, pb[m] + (unsigned)i * BPP));
                 }
                 V[i] = va;
                 V[g.W + i] = vb;
@@ -293,7 +300,9 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         }
     } else if (valid) {
         // odd H: the last pair's second row is outside the image (zero)
-        const float4 wa = rowW3[ra], wb = ra + 1 < g.H ? rowW3[ra + 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float4 wa = rowW3[ra], wb = ra + 1 < g.H ? rowW3[ra + 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        wa.x *= kLumaUnit<FMT>, wa.y *= kLumaUnit<FMT>, wa.z *= kLumaUnit<FMT>;
+        wb.x *= kLumaUnit<FMT>, wb.y *= kLumaUnit<FMT>, wb.z *= kLumaUnit<FMT>;
         const uint8_t *rowp[4];   // workgroup-uniform source row pointers
 #pragma unroll
         for (int d = 0; d < 4; ++d) rowp[d] = img + (unsigned)(wrap_near(ra - 1 + d, g.H, g.edge) * g.W * BPP);
@@ -313,7 +322,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
                 const int i = t + (h * UB + u) * T;
                 float l[4];
 #pragma unroll
-                for (int d = 0; d < 4; ++d) l[d] = luma_raw<FMT>(px[u][d]);
+                for (int d = 0; d < 4; ++d) l[d] = luma_units<FMT>(px[u][d]);
                 if (i < g.W) {
                     V[i] = wa.x * l[0] + wa.y * l[1] + wa.z * l[2];
                     V[g.W + i] = wb.x * l[1] + wb.y * l[2] + wb.z * l[3];
