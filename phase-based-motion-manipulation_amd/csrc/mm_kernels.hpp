@@ -331,10 +331,11 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         }
     }
     __syncthreads();
+    // all 8 colW3 loads in one batch (two batches of 4: one more dependent
+    // L2 round trip per pair, K1 +5 %)
     c2 v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        if (j == 4) __builtin_amdgcn_sched_barrier(0);     // two batches: bound VGPRs
         const int i = t + j * T - g.x0;                    // image column
         const int ic = min(max(i, 0), g.W - 1);
         float ya = 0.0f, yb = 0.0f;
@@ -356,7 +357,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         const bool in = valid && i >= 0 && i < g.W;
         v[j] = in ? mk(ya, yb) : mk(0.0f, 0.0f);
     }
-    c2 wb[16];
+    c2 wb[16];   // (issued at kernel start instead: K1 +5 %, registers held across the loads)
     preload_twiddles_wl<LOG2N>(wb, t, tw);
     __syncthreads();
     fft_dif<LOG2N, -1>(v, t, lds, wb);
