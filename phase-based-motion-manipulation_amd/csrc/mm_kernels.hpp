@@ -66,6 +66,7 @@ struct Spec {
 
 struct Blur5 { float w0, w1, w2; };  // taps at 0, +-1, +-2 texels
 
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
 template <int LOG2N> constexpr int fft_T() { return (1 << LOG2N) / 8; }
 template <int LOG2N> constexpr int groups_per_wg() { return fft_T<LOG2N>() >= 256 ? 1 : 256 / fft_T<LOG2N>(); }
 template <int LOG2N> constexpr int wg_threads() { return groups_per_wg<LOG2N>() * fft_T<LOG2N>(); }
@@ -820,25 +821,27 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     c2 ga[8];
     float gb[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     // (buffer loads: 32-bit offsets, and kept in order with the buffer stores)
+    // One buffer resource per column, its range the H image rows: row t + jT - y0
+    // at byte offset (t - y0) 8 + j T 8, and rows outside the image (negative
+    // offsets wrap to huge ones) fail the range check without any compare.
     auto load_g = [&](int fr, int t) {
         const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform
-        const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(G) + (size_t)gfr * g_stride, 0,
-                                                           (int)(g_stride * sizeof(c2)), 0x00020000);
+        const c2 *Gc = G + (size_t)gfr * g_stride;
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)f * g.Hg, 0,
+                                                           g.H * (int)sizeof(c2), 0x00020000);
+        const unsigned o0 = (unsigned)(t - g.y0) * 8u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int rr = t + j * T - g.y0;
-            const unsigned off = rr >= 0 && rr < g.H ? (unsigned)(f * g.Hg + rr) * 8u : 0x80000000u;
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, off, 0, 0);
+            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, o0 + (unsigned)(j * T * 8), 0, 0);
             ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
         }
         if constexpr (blk0) {   // column N/2 (real) for the packed group's block only
+            const auto nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)(N / 2) * g.Hg, 0,
+                                                               g.H * (int)sizeof(c2), 0x00020000);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int rr = t + j * T - g.y0;
-                const unsigned off = rr >= 0 && rr < g.H ? (unsigned)((N / 2) * g.Hg + rr) * 8u : 0x80000000u;
-                gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, off, 0, 0));
-            }
+            for (int j = 0; j < 8; ++j)
+                gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, o0 + (unsigned)(j * T * 8), 0, 0));
         }
     };
     // twiddle bases of both FFTs, loaded once: no loads inside a frame but G's
@@ -1091,16 +1094,35 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         // 1080p).  The GPW columns of the workgroup are transposed through LDS
         // (over the exchange buffers) and leave as one contiguous GPW*16-byte piece
         // per row pair; same-XCD workgroups complete the 128-B lines.
+        // Rows that never wrap (rb >= 0, rb + Hq <= N, every geometry but H
+        // close to N): list row k = t + jT - rb, staging slot s(k) = s(k0) + jT GPW
+        // (T a multiple of TK): one base and immediate offsets.
+        if (T % TK == 0 && g.rb >= 0 && g.rb + g.Hq <= N) {
+            const int k0 = t - g.rb;   // may be negative: floor division below
+            const int s0 = ((k0 >> ilog2c(TK)) * GPW) * TK + (k0 & (TK - 1));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-            if (valid && k < g.Hq) {
-                const int s = ((k / TK) * GPW) * TK + (k % TK);
-                if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
-                    stg[s] = mk(v[j].x, 0.0f);
-                    stgN[k] = v[j].y;
-                } else {
-                    stg[s + TK * grp] = v[j];
+            for (int j = 0; j < 8; ++j) {
+                if (valid && (unsigned)(k0 + j * T) < (unsigned)g.Hq) {
+                    if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
+                        stg[s0 + j * T * GPW] = mk(v[j].x, 0.0f);
+                        stgN[k0 + j * T] = v[j].y;
+                    } else {
+                        stg[s0 + j * T * GPW + TK * grp] = v[j];
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
+                if (valid && k < g.Hq) {
+                    const int s = ((k / TK) * GPW) * TK + (k % TK);
+                    if (packed) {
+                        stg[s] = mk(v[j].x, 0.0f);
+                        stgN[k] = v[j].y;
+                    } else {
+                        stg[s + TK * grp] = v[j];
+                    }
                 }
             }
         }
