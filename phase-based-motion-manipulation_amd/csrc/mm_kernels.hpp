@@ -878,7 +878,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         // every frame between the first-dispatched half of the grid and the
         // second keeps a pair in step (1082..1305 us).
         // Block 0 (the packed group's extra exchanges: the kernel's critical
-        // path, phase stamps) keeps the highest priority throughout.
+        // path, phase stamps) keeps the highest priority throughout (same-call
+        // A/B: ≈ 1 % over alternating it too, and over raising the packed group only).
         if (blk0) __builtin_amdgcn_s_setprio(3);
         else if ((fr ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
