@@ -61,6 +61,7 @@ struct mm_handle {
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
+    int k2_tail_pct;            // share of a batch's frames of k_cols's packed block run by k_cols_tail
     // mm_profile_begin/end: HIP events around each launch on its stream
     struct ProfRec { hipEvent_t a, b; int kernel, frames; };
     bool prof;
@@ -322,11 +323,23 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     ProfScope ps(h, s, MM_K_COLS, nframes);
     // per group: FFT exchange buffer + two per-bin tables (k_cols)
     const size_t lds = k2_lds_bytes<LOG2N>();
-#define MM_K2_LAUNCH(MODE)                                                                 \
-    hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, \
-                       h->d_G + h->g_stride * g_frame, h->g_stride, h->d_Q, h->q_stride, st_in, \
-                       st_out, nframes,                                                         \
-                       first_passthrough, h->geo, h->spec, h->d_tw)
+    // the packed block's last k frames go to k_cols_tail (k_cols's critical path)
+    int k = nframes >= 24 ? nframes * h->k2_tail_pct / 100 : 0;
+#ifdef MM_K2_STAMPS
+    k = 0;   // stamps are indexed by k_cols's blocks
+#endif
+    k = std::max(0, std::min(k, nframes - 2));
+    const c2 *G0 = h->d_G + h->g_stride * g_frame;
+#define MM_K2_LAUNCH(MODE)                                                                           \
+    do {                                                                                             \
+        hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, G0, \
+                           h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes, first_passthrough, \
+                           h->geo, h->spec, h->d_tw, nframes - k, k ? nullptr : st_out);           \
+        if (k)                                                                                       \
+            hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G0, \
+                               h->g_stride, h->d_Q, h->q_stride, st_out, nframes - k, h->geo, h->spec, \
+                               h->d_tw);                                                             \
+    } while (0)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
     else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB);
     else MM_K2_LAUNCH(MM_MODE_PYRAMID);
@@ -850,6 +863,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->blur = build_blur();
+    h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
 
     h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * g.Hg;

@@ -1138,7 +1138,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
     }
 #endif
-    if (valid) {
+    if (valid && state_out) {   // (k_cols_tail: only the last frame's workgroup)
         if (packed) {
             // column 0 from bins fy <= N/2 (j < 4, and N/2 at thread 0), column
             // N/2 from bins N - fy (j >= 4) and thread 0's two real bins; the
@@ -1175,17 +1175,38 @@ template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
             const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
-            Geo g, Spec sp, const c2 *__restrict__ tw)
+            Geo g, Spec sp, const c2 *__restrict__ tw, int nframes_blk0, c2 *state_out_blk0)
 {
     // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
     // are merged in one L2 (split over XCDs they left as partial-line writes)
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    if (blk == 0)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Q, q_stride, state_in, state_out, nframes,
+    if (blk == 0)   // the packed block stops nframes_blk0 frames in (k_cols_tail)
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Q, q_stride, state_in, state_out_blk0, nframes_blk0,
                                        first_passthrough, g, sp, tw, blk);
     else
         k_cols_body<LOG2N, MODE, false>(G, g_stride, Q, q_stride, state_in, state_out, nframes,
                                         first_passthrough, g, sp, tw, blk);
+}
+
+// The packed block's last k frames, one workgroup per frame, after k_cols.
+// Block 0 carries the packed group's extra exchanges and is k_cols's critical
+// path, so the other blocks would idle at the end of the launch (rocprofv3:
+// k_cols 1,016 us per 100 frames alone; 939 us + 24.5 us of k_cols_tail with
+// the last 30 frames moved, 940 + 24.6 with 45: the 30 % default is past the
+// point where block 0 stops being the critical path).  The state is a
+// pure function of the previous input frame (.cs:142), so workgroup i starts
+// from frame f0 + i - 1 as a passthrough frame (its forward FFT sets F_{t-1}
+// exactly as the frame loop would: bitwise the same outputs) and then runs
+// frame f0 + i.  The last one writes the columns' state.
+template <int LOG2N, int MODE>
+__global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
+void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, c2 *state_out, int f0,
+                 Geo g, Spec sp, const c2 *__restrict__ tw)
+{
+    const int fr = f0 + (int)blockIdx.x;   // >= 1
+    k_cols_body<LOG2N, MODE, true>(G + (size_t)(fr - 1) * g_stride, g_stride, Q + (size_t)(fr - 1) * q_stride,
+                                   q_stride, nullptr, blockIdx.x + 1 == gridDim.x ? state_out : nullptr, 2, 1,
+                                   g, sp, tw, 0);
 }
 
 // =========================================================================

@@ -435,3 +435,20 @@ def test_odd_1919x1079_u8_stream():
     assert np.array_equal(got[0], fr[0])
     T.assert_close_u8(np.stack(got[1:]), np.stack(ref[1:]))
 
+
+
+
+# ---- k_cols_tail: the packed block's last frames as one-frame workgroups ----
+@pytest.mark.parametrize("W,H,n,batch,tail", [(1920, 1080, 50, 25, "12"), (640, 360, 60, 30, "25"),
+                                              (256, 256, 72, 24, "50")])
+def test_k2_tail_bitwise_equals_single_launch(W, H, n, batch, tail, monkeypatch):
+    """Frames handed from k_cols's packed block to k_cols_tail (which restarts
+    from the previous input frame) give bitwise the single-launch outputs; the
+    stream spans several batches, so the state the tail writes is used next."""
+    fr = T.synth(W, H, n, fmt="u8")
+    monkeypatch.setenv("MM_K2_TAIL", "0")
+    a = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
+    monkeypatch.setenv("MM_K2_TAIL", tail)
+    b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
