@@ -325,9 +325,6 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     const size_t lds = k2_lds_bytes<LOG2N>();
     // the packed block's last k frames go to k_cols_tail (k_cols's critical path)
     int k = nframes >= 24 ? nframes * h->k2_tail_pct / 100 : 0;
-#ifdef MM_K2_STAMPS
-    k = 0;   // stamps are indexed by k_cols's blocks
-#endif
     k = std::max(0, std::min(k, nframes - 2));
     const c2 *G0 = h->d_G + h->g_stride * g_frame;
 #define MM_K2_LAUNCH(MODE)                                                                           \

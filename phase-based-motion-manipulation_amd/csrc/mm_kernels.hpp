@@ -1134,7 +1134,9 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 #ifdef MM_K2_STAMPS
     st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
     if (threadIdx.x % 64 == 0) {
-        const int w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        // k_cols_tail's workgroups (one per frame) after k_cols's 4096 waves
+        const int w = (blk0 && nframes == 2 && first_passthrough && gridDim.x < 512 ? 4096 : 0) +
+                      blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
         for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
     }
 #endif
