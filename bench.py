@@ -57,7 +57,9 @@ def compulsory_bytes(W, H, N, frames, b_in=4, b_out=4):
     return {"k_rows_fwd": frames * (W * H * b_in + F * H * 8),
             "k_cols": frames * (F * H * 8 + F * Hq * 8) + 2 * F * N * 8,
             "k_rows_inv": frames * (F * Hq * 8 + Hn * W * 4),
-            "k_compose": frames * (Hn * W * 4 + W * H * (b_in + b_out))}
+            "k_compose": frames * (Hn * W * 4 + W * H * (b_in + b_out)),
+            # K3 + K4 fused (even sizes): Q once, the input for I/Q, the output
+            "k_rows_inv_compose": frames * (F * Hq * 8 + W * H * (b_in + b_out))}
 
 
 def parse():
@@ -326,23 +328,26 @@ def drop_in_per_frame(mm355, torch, params, W, H, frames, local, count):
                        "on its stream"}
 
 
-def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None):
+def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None, ran=None):
     """Frame-level HBM roofline: the design's compulsory bytes per output
-    frame (the four kernels' compulsory_bytes() at this batch size, per frame)
-    x frames/s per GPU vs 8 TB/s; PMC bytes per frame (profiles/traffic.json,
-    rocprofv3 FETCH_SIZE/WRITE_SIZE) beside them."""
+    frame (compulsory_bytes() of the kernels that ran, at this batch size, per
+    frame) x frames/s per GPU vs 8 TB/s; PMC bytes per frame
+    (profiles/traffic.json, rocprofv3 FETCH_SIZE/WRITE_SIZE) beside them."""
     cb = compulsory_bytes(W, H, N, batch)
-    per_frame = sum(cb.values()) / batch
+    if ran is None:
+        ran = [k for k in cb if k != "k_rows_inv_compose"]
+    per_frame = sum(cb[k] for k in ran if k in cb) / batch
     rec = {"bytes_per_frame": int(per_frame),
            "achieved_GBps": round(per_frame * fps_per_gpu / 1e9, 1),
            "peak": HBM_PEAK_GBPS, "frac": round(per_frame * fps_per_gpu / 1e9 / HBM_PEAK_GBPS, 4),
            "pmc_bytes_per_frame": None, "pmc_ratio": None,
-           "note": "compulsory bytes of K1+K2+K3+K4 per frame (DESIGN.md §5) x frames/s per GPU"}
+           "note": "compulsory bytes per frame of the kernels that ran (" + "+".join(ran) +
+                   "; DESIGN.md §5) x frames/s per GPU"}
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            pmc = sum(k["hbm_bytes_per_frame"] for k in tj["kernels"].values())
+            pmc = sum(tj["kernels"][k]["hbm_bytes_per_frame"] for k in ran)
             rec["pmc_bytes_per_frame"] = int(pmc)
             rec["pmc_ratio"] = round(pmc / per_frame, 4)
             rec["pmc_source"] = "profiles/traffic.json"
@@ -525,7 +530,8 @@ def main():
                      "bytes_model": "compulsory bytes of the dominant kernel (DESIGN.md §5); "
                                     "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch",
                      "compute": valu},
-        "frame_roofline": (frame_roofline(W, H, N, fps / world, batch) if not steer else None),
+        "frame_roofline": (frame_roofline(W, H, N, fps / world, batch, ran=list(kern))
+                           if not steer else None),
         "survey_model": {"bytes_per_frame": B_survey,
                          "equivalent_GBps_per_gpu": round(B_survey * fps / world / 1e9, 1),
                          "note": "SURVEY.md §8(d) B=W*H*(2b_in+b_out)+6*N^2*8 charges dense "

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 6
+#define MM_ABI_VERSION 7
 
 /* error codes */
 #define MM_OK               0
@@ -192,7 +192,8 @@ int mm_abi_version(void);
 #define MM_K_COLS     1   /* K2: column FFT + pyramid phase op + IFFT  */
 #define MM_K_ROWS_INV 2   /* K3: row C2R IFFT + |z| + horizontal blur    */
 #define MM_K_COMPOSE  3   /* K4: vertical blur + YIQ recombine + RGB + crop */
-#define MM_K_COUNT    4
+#define MM_K_ROWS_INV_COMPOSE 4   /* K3 + K4 fused (even sizes, N - H >= 4)  */
+#define MM_K_COUNT    5
 int mm_profile_begin(mm_handle *h);
 /* Waits for the recorded events; ms[k] = summed device ms, launches[k],
  * frames[k] = frames processed by kernel k, k < MM_K_COUNT (arrays of

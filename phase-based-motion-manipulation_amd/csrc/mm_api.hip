@@ -62,6 +62,7 @@ struct mm_handle {
     size_t stage_bytes;
     bool has_state;
     int k2_tail_pct;            // share of a batch's frames of k_cols's packed block run by k_cols_tail
+    int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused)
     // mm_profile_begin/end: HIP events around each launch on its stream
     struct ProfRec { hipEvent_t a, b; int kernel, frames; };
     bool prof;
@@ -348,12 +349,40 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
 static int launch_k4(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, int nframes,
                      int fmt, hipStream_t s);
 
+// k_rows_inv_compose's geometry: even sizes whose quads tile the rows (W % 8 == 0
+// puts x0 on a multiple of 4), the horizontal blur's float4 taps inside the
+// canvas, and no vertical blur tap wrapping (list row of output row i + v is i + v)
+static bool k34_fits(const mm_handle *h)
+{
+    const Geo &g = h->geo;
+    return h->k34_rows >= 4 && !g.ox && !g.oy && g.W % 8 == 0 && g.x0 >= 4 && g.x0 % 4 == 0 &&
+           g.x0 + g.W + 4 <= g.N && g.N - g.H >= 4 && g.Hn == g.H + 4 && g.rb == g.y0 - 2 &&
+           2 * (g.N / 8) >= g.W / 4;
+}
+
 template <int LOG2N>
 static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, int nframes,
                      int fmt, hipStream_t s)
 {
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
+    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    if (LOG2N <= 11 && k34_fits(h)) {   // K3 + K4 fused: Yh stays on chip
+        const int R = h->k34_rows, strips = (h->H + R - 1) / R, steps = R / 4 + 1;
+        const size_t lds = sizeof(c2) * 2 * lds_complex<(1 << LOG2N)>();
+        const dim3 grid((unsigned)(strips * nout)), block(2 * fft_T<LOG2N>());
+        ProfScope ps(h, s, MM_K_ROWS_INV_COMPOSE, nout);
+        if (fmt == MM_RGBA8)
+            hipLaunchKernelGGL((k_rows_inv_compose<LOG2N, 0>), grid, block, lds, s, h->d_Q, h->q_stride,
+                               in, out, fb, frame0, strips, steps, h->geo, h->blur, h->d_col3,
+                               h->d_row3, h->d_tw);
+        else
+            hipLaunchKernelGGL((k_rows_inv_compose<LOG2N, 1>), grid, block, lds, s, h->d_Q, h->q_stride,
+                               in, out, fb, frame0, strips, steps, h->geo, h->blur, h->d_col3,
+                               h->d_row3, h->d_tw);
+        HIPCHK(hipGetLastError());
+        return MM_OK;
+    }
     const int ppf = h->geo.Hq / 2;   // whole Q tiles (k_rows_inv)
     const int total = ppf * nout;
     const int gpw = k3_groups<LOG2N>();
@@ -861,6 +890,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
+    h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : 64;
 
     h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * g.Hg;

@@ -177,11 +177,15 @@ template <> struct Pix<0> {           // RGBA8 UNORM
                            (float)((u >> 16) & 255u) * s, (float)(u >> 24) * s);
     }
     __device__ static float4 load(const uint8_t *base, size_t i) { return cvt(raw(base, i)); }
-    __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
+    __device__ static uint32_t pack(float r, float g, float b)
     {
         uint32_t R = (uint32_t)(r * 255.0f + 0.5f), G = (uint32_t)(g * 255.0f + 0.5f),
                  B = (uint32_t)(b * 255.0f + 0.5f);
-        st_off<uint32_t>(base, i * 4u, R | (G << 8) | (B << 16) | (255u << 24));
+        return R | (G << 8) | (B << 16) | (255u << 24);
+    }
+    __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
+    {
+        st_off<uint32_t>(base, i * 4u, pack(r, g, b));
     }
 };
 template <> struct Pix<1> {           // RGBA32F
@@ -1406,6 +1410,172 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
             const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
             const float bb = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
             Pix<FMT>::store(outp + (unsigned)(i * g.W * Pix<FMT>::bpp), (unsigned)X, rr, gg, bb);
+        }
+    }
+}
+
+// =========================================================================
+// K34: K3 + K4 fused (even W, H with W % 8 == 0, N - W >= 8, N - H >= 4)
+// =========================================================================
+// One workgroup of two FFT groups (2T = N/4 threads >= W/4 column quads) walks
+// a strip of R = 4 (steps - 1) output rows of one frame top to bottom.  Step s
+// inverse-transforms the Q list-row pairs i0/2 + 2s + {0, 1} (list rows
+// i0+4s .. i0+4s+3) exactly as k_rows_inv does, blurs them horizontally from
+// LDS, and thread q keeps the blurred values of its quad X = 4q .. 4q+3 in
+// registers.  Output row i reads list rows i .. i+4 (rb = y0 - 2 and no row of
+// the vertical blur wraps when N - H >= 4), so from step 1 on the 8 list rows
+// in registers are the taps of output rows i0+4s-4 .. i0+4s-1, composed as
+// k_compose does (same expressions).  Yh never goes through HBM: the frame
+// saves its write and re-read (2 x 4 Hn W bytes); a strip re-transforms 4
+// halo rows (4 / R more Q reads and FFT work).
+template <int LOG2N, int FMT>
+__global__ __launch_bounds__(2 * fft_T<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
+void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
+                        const uint8_t *__restrict__ frames_in, uint8_t *__restrict__ frames_out,
+                        size_t frame_bytes, int frame0, int strips, int steps, Geo g, Blur5 bw,
+                        const float4 *__restrict__ colW3, const float4 *__restrict__ rowW3,
+                        const c2 *__restrict__ tw)
+{
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), TK = q_tile<LOG2N>();
+    using raw_t = typename Pix<FMT>::raw_t;
+    constexpr unsigned bpp = Pix<FMT>::bpp;
+    extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
+    const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
+    const int t = threadIdx.x % T;
+    c2 *lds = lds_all + grp * lds_complex<N>();
+    const float *raw_all = reinterpret_cast<const float *>(lds_all);
+    constexpr int GROUP_FLOATS = 2 * lds_complex<N>();
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int frame = frame0 + b / strips;
+    const int i0 = (b % strips) * 4 * (steps - 1);
+    const c2 *Qf = Q + (size_t)frame * q_stride;
+    const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
+    uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
+
+    const int q = threadIdx.x;
+    const bool vq = 4 * q < g.W;
+    const int X = vq ? 4 * q : g.W - 4;     // clamped quad (loads stay in the image)
+    const unsigned cl = (unsigned)wrap_near(X - 1, g.W, g.edge);
+    const unsigned cr = (unsigned)wrap_near(X + 4, g.W, g.edge);
+    // horizontally combined I/Q of one source row for the quad (k_compose's
+    // staged 3-tap combine over columns X-1 .. X+4)
+    auto chroma_row = [&](int i, float (&hi)[4], float (&hq)[4]) {
+        const int row = wrap_near(min(i, g.H), g.H, g.edge);
+        const unsigned base = (unsigned)(row * g.W);
+        raw_t p[6];
+        p[0] = ld_off<raw_t>(img, (base + cl) * bpp);
+        if constexpr (FMT == 0) {
+            const uint4 m = ld_off<uint4>(img, (base + (unsigned)X) * bpp);
+            p[1] = m.x; p[2] = m.y; p[3] = m.z; p[4] = m.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) p[1 + k] = ld_off<raw_t>(img, (base + (unsigned)X + k) * bpp);
+        }
+        p[5] = ld_off<raw_t>(img, (base + cr) * bpp);
+        float2 a[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[k] = chroma_iq<FMT>(p[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 wc = colW3[X + k];
+            hi[k] = wc.x * a[k].x + wc.y * a[k + 1].x + wc.z * a[k + 2].x;
+            hq[k] = wc.x * a[k].y + wc.y * a[k + 1].y + wc.z * a[k + 2].y;
+        }
+    };
+
+    float yw[8][4];            // list rows i0+4s-4 .. i0+4s+3 of the quad (blurred horizontally)
+    float hi[6][4], hq[6][4];  // combined I/Q of source rows i0+4s-5 .. i0+4s
+    chroma_row(i0 - 1, hi[4], hq[4]);
+    chroma_row(i0, hi[5], hq[5]);
+    for (int s = 0; s < steps; ++s) {
+        // ---- K3 on list-row pair i0/2 + 2s + grp (zero beyond Hn) ----
+        const int ka = i0 + 4 * s + 2 * grp;
+        const bool valid = ka < g.Hn;
+        const int kl = valid ? ka : 0;
+        const float4 *Qp = reinterpret_cast<const float4 *>(Qf + (size_t)(kl / TK) * g.Qs * TK + (kl % TK));
+        float4 qv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int fq = t + j * T;
+            const int ff = fq > N / 2 ? N - fq : fq;
+            qv[j] = Qp[(size_t)ff * (TK / 2)];
+        }
+        c2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int fq = t + j * T;
+            const bool mirror = fq > N / 2;
+            const int ff = mirror ? N - fq : fq;
+            float4 qq = qv[j];
+            if (ff == 0 || ff == N / 2) { qq.y = 0.0f; qq.w = 0.0f; }
+            if (mirror) { qq.y = -qq.y; qq.w = -qq.w; }
+            v[j] = valid ? mk(qq.x - qq.w, qq.y + qq.z) : mk(0.0f, 0.0f);
+        }
+        fft_regs<LOG2N, +1>(v, t, lds, tw);
+        float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows ka, ka+1
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            raw[t + j * T] = fabsf(v[j].x);
+            raw[N + t + j * T] = fabsf(v[j].y);
+        }
+        __syncthreads();
+        // ---- horizontal blur of the 4 new list rows (k_rows_inv's float4 form) ----
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float *rw = raw_all + (r >> 1) * GROUP_FLOATS + (r & 1) * N + g.x0 + X;
+            const float4 *r4 = reinterpret_cast<const float4 *>(rw);
+            const float4 A = r4[-1], B = r4[0], C = r4[1];
+            yw[4 + r][0] = bw.w0 * B.x + bw.w1 * (A.w + B.y) + bw.w2 * (A.z + B.z);
+            yw[4 + r][1] = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
+            yw[4 + r][2] = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
+            yw[4 + r][3] = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
+        }
+        __syncthreads();   // LDS free for the next step's FFT
+        if (s > 0) {
+            // ---- K4 on output rows i0+4s-4 .. i0+4s-1 ----
+#pragma unroll
+            for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hi[2 + r], hq[2 + r]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + 4 * s - 4 + r;
+                if (vq && i < g.H) {
+                    const float4 wr = rowW3[i];
+                    float rr[4], gg[4], bb[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float ci = wr.x * hi[r][k] + wr.y * hi[r + 1][k] + wr.z * hi[r + 2][k];
+                        const float cq = wr.x * hq[r][k] + wr.y * hq[r + 1][k] + wr.z * hq[r + 2][k];
+                        const float yb = bw.w0 * yw[r + 2][k] + bw.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
+                                         bw.w2 * (yw[r][k] + yw[r + 4][k]);
+                        rr[k] = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
+                        gg[k] = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
+                        bb[k] = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
+                    }
+                    const unsigned o = (unsigned)(i * g.W + X);
+                    if constexpr (FMT == 0) {
+                        uint4 px;
+                        px.x = Pix<0>::pack(rr[0], gg[0], bb[0]);
+                        px.y = Pix<0>::pack(rr[1], gg[1], bb[1]);
+                        px.z = Pix<0>::pack(rr[2], gg[2], bb[2]);
+                        px.w = Pix<0>::pack(rr[3], gg[3], bb[3]);
+                        st_off<uint4>(outp, o * 4u, px);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) Pix<1>::store(outp, o + k, rr[k], gg[k], bb[k]);
+                    }
+                }
+            }
+        }
+        // ---- slide: keep list rows i0+4s .. +3 and source rows i0+4s-1, i0+4s
+        // (after step 0: the primed rows i0-1, i0) ----
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) yw[r][k] = yw[4 + r][k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            hi[0][k] = hi[4][k]; hq[0][k] = hq[4][k];
+            hi[1][k] = hi[5][k]; hq[1][k] = hq[5][k];
         }
     }
 }

@@ -21,7 +21,8 @@ FILTER_DIFF = 0
 FILTER_IIR = 1
 FRAMES_ON_DEVICE = 1
 
-KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv", "k_compose")   # MM_K_* ids 0..3
+KERNELS = ("k_rows_fwd", "k_cols", "k_rows_inv", "k_compose",
+           "k_rows_inv_compose")   # MM_K_* ids 0..4
 
 ERRORS = {0: "MM_OK", -1: "MM_ERR_INVALID", -2: "MM_ERR_UNSUPPORTED", -3: "MM_ERR_HIP",
           -4: "MM_ERR_NO_DEVICE", -5: "MM_ERR_OOM", -6: "MM_ERR_NO_STATE"}
@@ -74,7 +75,7 @@ class Params(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 6   # include/mm.h MM_ABI_VERSION
+ABI_VERSION = 7   # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):

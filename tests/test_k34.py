@@ -1,0 +1,99 @@
+"""K3 + K4 fused (k_rows_inv_compose, csrc/mm_kernels.hpp) against the
+unfused k_rows_inv + k_compose pair and against the oracle.
+
+The fused kernel walks strips of MM_K34_ROWS output rows (read at mm_create;
+0 selects the unfused pair).  Geometries: several strips with a partial last
+strip, strips taller than the image, both edge modes (the chroma rows wrap or
+clamp at the image edges), RGBA32F and RGBA8, the rows of a 1080p frame.
+The same expressions in the same order run in both forms, so they must agree
+bitwise; the oracle bars are tests/mmtest.py's.
+"""
+import os
+import numpy as np
+import pytest
+
+import mmtest as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_env(rows, *args, **kw):
+    old = os.environ.get("MM_K34_ROWS")
+    os.environ["MM_K34_ROWS"] = str(rows)
+    try:
+        return T.gpu_run(*args, **kw)
+    finally:
+        if old is None:
+            del os.environ["MM_K34_ROWS"]
+        else:
+            os.environ["MM_K34_ROWS"] = old
+
+
+def _kernels_ran(rows, W, H):
+    """Names of the K3/K4 kernels one 2-frame stream launches at this strip size."""
+    import torch
+    import mm355
+    old = os.environ.get("MM_K34_ROWS")
+    os.environ["MM_K34_ROWS"] = str(rows)
+    try:
+        h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
+    finally:
+        if old is None:
+            del os.environ["MM_K34_ROWS"]
+        else:
+            os.environ["MM_K34_ROWS"] = old
+    fr = torch.zeros((2, H, W, 4), dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(fr)
+    h.profile_begin()
+    h.process_stream(fr, out, 2, mm355.RGBA8)
+    torch.cuda.synchronize()
+    prof = h.profile_end()
+    h.close()
+    return {k for k, (ms, n, f) in prof.items() if n}
+
+
+def test_fused_path_is_selected():
+    assert "k_rows_inv_compose" in _kernels_ran(64, 200, 120)
+    assert "k_rows_inv_compose" not in _kernels_ran(0, 200, 120)
+    # W = 64 at N = 64: x0 = 0 leaves no room for the horizontal blur's taps
+    assert "k_rows_inv_compose" not in _kernels_ran(64, 64, 48)
+
+
+@pytest.mark.parametrize("W,H,rows,edge,fmt", [
+    (200, 120, 64, 0, "f32"), (200, 120, 8, 1, "f32"), (200, 118, 4, 0, "u8"),
+    (240, 136, 12, 1, "u8"), (120, 200, 32, 0, "f32"), (504, 250, 16, 1, "u8")])
+def test_fused_equals_unfused_bitwise(W, H, rows, edge, fmt):
+    fr = T.synth(W, H, 5, fmt=fmt)
+    a = _run_env(rows, W, H, fr, 5, 25.0, edge, mode="stream")
+    b = _run_env(0, W, H, fr, 5, 25.0, edge, mode="stream")
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("W,H,rows,edge", [(200, 120, 16, 0), (240, 136, 64, 1)])
+def test_fused_vs_oracle(W, H, rows, edge):
+    fr = T.synth(W, H, 4)
+    ref = T.oracle_run(W, H, fr, 5, 25.0, edge)
+    got = _run_env(rows, W, H, fr, 5, 25.0, edge)
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r)
+
+
+def test_fused_equals_unfused_1080p_u8():
+    W, H = 1920, 1080
+    fr = T.synth(W, H, 3, fmt="u8")
+    a = _run_env(64, W, H, fr, 5, 25.0, 0, mode="stream")
+    b = _run_env(0, W, H, fr, 5, 25.0, 0, mode="stream")
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_fused_standard_mode():
+    W, H = 200, 120
+    fr = T.synth(W, H, 4)
+    std = {"apply": True}
+    a = _run_env(16, W, H, fr, 5, 25.0, 0, mode="stream", standard=std)
+    b = _run_env(0, W, H, fr, 5, 25.0, 0, mode="stream", standard=std)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
