@@ -19,12 +19,19 @@ def test_metric_matches_baseline_json_at_default_config():
 
 def test_frame_roofline_is_sum_of_compulsory_bytes():
     W, H, N, C = 1920, 1080, 2048, 100
-    r = bench.frame_roofline(W, H, N, 10000.0, C)
-    per = sum(bench.compulsory_bytes(W, H, N, C).values()) / C
-    assert r["bytes_per_frame"] == int(per)
-    assert abs(r["frac"] - per * 1e4 / 8e12) < 1e-4
-    # 1080p RGBA8: ~77-79 MB per frame, far below SURVEY's 226 MB
-    assert 70e6 < per < 85e6
+    cb = bench.compulsory_bytes(W, H, N, C)
+    unfused = ["k_rows_fwd", "k_cols", "k_rows_inv", "k_compose"]
+    fused = ["k_rows_fwd", "k_cols", "k_rows_inv_compose"]
+    for ran, lo, hi in ((unfused, 70e6, 85e6), (fused, 55e6, 65e6)):
+        r = bench.frame_roofline(W, H, N, 10000.0, C, ran=ran)
+        per = sum(cb[k] for k in ran) / C
+        assert r["bytes_per_frame"] == int(per)
+        assert abs(r["frac"] - per * 1e4 / 8e12) < 1e-4
+        # 1080p RGBA8: ~77 MB per frame through Yh, ~61 MB with K3+K4 fused
+        # (DESIGN.md §5), far below SURVEY's 226 MB
+        assert lo < per < hi
+    # default: the unfused set
+    assert bench.frame_roofline(W, H, N, 1e4, C)["bytes_per_frame"] == int(sum(cb[k] for k in unfused) / C)
 
 
 def test_available_cpus_positive():
