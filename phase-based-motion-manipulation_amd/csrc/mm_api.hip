@@ -62,7 +62,8 @@ struct mm_handle {
     size_t stage_bytes;
     bool has_state;
     int k2_tail_pct;            // share of a batch's frames of k_cols's packed block run by k_cols_tail
-    int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused)
+    int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused;
+                                // -1: by the launch's frame count, k34_strip_rows)
     // mm_profile_begin/end: HIP events around each launch on its stream
     struct ProfRec { hipEvent_t a, b; int kernel, frames; };
     bool prof;
@@ -355,9 +356,22 @@ static int launch_k4(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
 static bool k34_fits(const mm_handle *h)
 {
     const Geo &g = h->geo;
-    return h->k34_rows >= 4 && !g.ox && !g.oy && g.W % 8 == 0 && g.x0 >= 4 && g.x0 % 4 == 0 &&
+    return !g.ox && !g.oy && g.W % 8 == 0 && g.x0 >= 4 && g.x0 % 4 == 0 &&
            g.x0 + g.W + 4 <= g.N && g.N - g.H >= 4 && g.Hn == g.H + 4 && g.rb == g.y0 - 2 &&
            2 * (g.N / 8) >= g.W / 4;
+}
+
+// Strip height of one k_rows_inv_compose launch over nout frames.  A strip is
+// one workgroup walking its rows in sequence, so a launch needs many strips:
+// about 4 workgroups per CU (H nout / R >= 1024) with R <= 64, and the unfused
+// pair (0) when that would take strips under 16 rows (the one-frame drop-in
+// call: K3 + K4 spread one frame over thousands of workgroups).  MM_K34_ROWS
+// forces a strip height (0: unfused).
+static int k34_strip_rows(const mm_handle *h, int nout)
+{
+    if (h->k34_rows >= 0) return h->k34_rows;
+    const int R = std::min(64, (int)((long long)h->H * nout / 1024) / 4 * 4);
+    return R >= 16 ? R : 0;
 }
 
 template <int LOG2N>
@@ -367,8 +381,9 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-    if (LOG2N <= 11 && k34_fits(h)) {   // K3 + K4 fused: Yh stays on chip
-        const int R = h->k34_rows, strips = (h->H + R - 1) / R, steps = R / 4 + 1;
+    const int R = k34_strip_rows(h, nout);
+    if (LOG2N <= 11 && R >= 4 && k34_fits(h)) {   // K3 + K4 fused: Yh stays on chip
+        const int strips = (h->H + R - 1) / R, steps = R / 4 + 1;
         const size_t lds = sizeof(c2) * 2 * lds_complex<(1 << LOG2N)>();
         const dim3 grid((unsigned)(strips * nout)), block(2 * fft_T<LOG2N>());
         ProfScope ps(h, s, MM_K_ROWS_INV_COMPOSE, nout);
@@ -890,7 +905,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
-    h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : 64;
+    h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
 
     h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * g.Hg;

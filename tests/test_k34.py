@@ -29,23 +29,29 @@ def _run_env(rows, *args, **kw):
             os.environ["MM_K34_ROWS"] = old
 
 
-def _kernels_ran(rows, W, H):
-    """Names of the K3/K4 kernels one 2-frame stream launches at this strip size."""
+def _kernels_ran(rows, W, H, n=2, batch=None):
+    """Names of the kernels an n-frame stream launches at this strip size
+    (rows None: the library's own choice by batch size)."""
     import torch
     import mm355
     old = os.environ.get("MM_K34_ROWS")
-    os.environ["MM_K34_ROWS"] = str(rows)
+    if rows is None:
+        os.environ.pop("MM_K34_ROWS", None)
+    else:
+        os.environ["MM_K34_ROWS"] = str(rows)
     try:
         h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
     finally:
         if old is None:
-            del os.environ["MM_K34_ROWS"]
+            os.environ.pop("MM_K34_ROWS", None)
         else:
             os.environ["MM_K34_ROWS"] = old
-    fr = torch.zeros((2, H, W, 4), dtype=torch.uint8, device="cuda")
+    if batch:
+        h.set_batch(batch)
+    fr = torch.zeros((n, H, W, 4), dtype=torch.uint8, device="cuda")
     out = torch.empty_like(fr)
     h.profile_begin()
-    h.process_stream(fr, out, 2, mm355.RGBA8)
+    h.process_stream(fr, out, n, mm355.RGBA8)
     torch.cuda.synchronize()
     prof = h.profile_end()
     h.close()
@@ -57,6 +63,14 @@ def test_fused_path_is_selected():
     assert "k_rows_inv_compose" not in _kernels_ran(0, 200, 120)
     # W = 64 at N = 64: x0 = 0 leaves no room for the horizontal blur's taps
     assert "k_rows_inv_compose" not in _kernels_ran(64, 64, 48)
+
+
+def test_strip_policy_by_batch():
+    """Default strip height: fused for many-frame batches, the unfused pair for
+    the one-frame drop-in call (a strip is one sequential workgroup)."""
+    assert "k_rows_inv_compose" not in _kernels_ran(None, 1920, 1080, n=2, batch=1)
+    assert "k_rows_inv_compose" not in _kernels_ran(None, 1920, 1080, n=2, batch=8)
+    assert "k_rows_inv_compose" in _kernels_ran(None, 1920, 1080, n=40, batch=100)
 
 
 @pytest.mark.parametrize("W,H,rows,edge,fmt", [
