@@ -8,6 +8,6 @@ python3 tools/valu_summary.py gpurun_out/${TAG}_st_1,gpurun_out/${TAG}_st_2 gpur
 python3 -c "
 import json,sys
 v=json.load(open(sys.argv[1])); s=json.load(open(sys.argv[2]))
-for k in ('k_rows_fwd','k_cols','k_rows_inv','k_compose'):
+for k in ('k_rows_fwd','k_cols','k_rows_inv','k_compose','k_rows_inv_compose'):
     print(k, {a: v[k][a] for a in ('valu_insts_per_launch','launch_s','clock_GHz','valu_busy')}, {a: s[k].get(a) for a in ('frac_SQ_WAIT_ANY','frac_SQ_WAIT_INST_ANY','frac_SQ_ACTIVE_INST_ANY','lds_conflict_frac')})
 " gpurun_out/${TAG}_valu.json gpurun_out/${TAG}_st_summary.json

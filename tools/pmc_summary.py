@@ -17,7 +17,8 @@ import sys
 from collections import defaultdict
 
 # dominant (read width, write width) in bytes per lane, per kernel
-WIDTHS = {"k_rows_fwd": (4, 16), "k_cols": (8, 8), "k_rows_inv": (16, 4), "k_compose": (4, 4)}
+WIDTHS = {"k_rows_fwd": (4, 16), "k_cols": (8, 8), "k_rows_inv": (16, 4), "k_compose": (4, 4),
+          "k_rows_inv_compose": (16, 16)}
 CAL_BYTES = 512 << 20
 
 
