@@ -284,7 +284,14 @@ template <int LOG2N> static size_t lds_fft_bytes()
 template <int LOG2N>
 static int set_attrs(int W)
 {
-    (void)W;   // every kernel stays within the default 64 KiB dynamic LDS
+    (void)W;   // every other kernel stays within the default 64 KiB dynamic LDS
+    if constexpr (LOG2N == 12) {   // k_rows_inv_compose: two 4096-point groups, 73.7 KB
+        const int lds = (int)(sizeof(c2) * 2 * lds_complex<4096>());
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, 0>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, 1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    }
     return MM_OK;
 }
 
@@ -382,7 +389,7 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     if (nout <= 0) return MM_OK;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     const int R = k34_strip_rows(h, nout);
-    if (LOG2N <= 11 && R >= 4 && k34_fits(h)) {   // K3 + K4 fused: Yh stays on chip
+    if (R >= 4 && k34_fits(h)) {   // K3 + K4 fused: Yh stays on chip
         const int strips = (h->H + R - 1) / R, steps = R / 4 + 1;
         const size_t lds = sizeof(c2) * 2 * lds_complex<(1 << LOG2N)>();
         const dim3 grid((unsigned)(strips * nout)), block(2 * fft_T<LOG2N>());

@@ -111,3 +111,15 @@ def test_fused_standard_mode():
     b = _run_env(0, W, H, fr, 5, 25.0, 0, mode="stream", standard=std)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.slow
+def test_fused_equals_unfused_2160p_u8():
+    """N = 4096: two 512-thread groups per workgroup (1,024 threads) and 73.7 KB
+    of dynamic LDS (hipFuncSetAttribute at mm_create)."""
+    W, H = 3840, 2160
+    fr = T.synth(W, H, 3, fmt="u8")
+    a = _run_env(64, W, H, fr, 6, 25.0, 0, mode="stream")
+    b = _run_env(0, W, H, fr, 6, 25.0, 0, mode="stream")
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
