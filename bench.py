@@ -11,8 +11,13 @@ device and resident in HBM before timing.
 N > 1 (launched by torch.distributed.run, one rank per GPU): the stream is
 frame-sharded: each step rank g processes its own contiguous
 chunk and one RCCL ring shift carries the chunk-boundary temporal state
-(`--mode ring`, default).  `--mode replicas` runs independent streams
-(BASELINE configs[4]).  Weak scaling either way.
+(`--mode ring`, default).  The ring is the C host's (`--ring-impl c`,
+default: include/mm_ring.h, lib/libmm_ring.so, its own RCCL communicator;
+torch.distributed over gloo only hands rank 0's ring id to the others and
+runs the timing barrier and max); `--ring-impl torch` is the Python
+ShardedStream over torch.distributed (the gloo rehearsal uses it).
+`--mode replicas` runs independent streams (BASELINE configs[4]).  Weak
+scaling either way.
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` (dominant kernel, HIP-event time measured on its launch stream
@@ -54,8 +59,11 @@ def compulsory_bytes(W, H, N, frames, b_in=4, b_out=4):
     columns, Hn = H+4 rows kept for the crop + vertical blur."""
     F, Hn = N // 2 + 1, min(H + 4, N)
     Hq = Hn + (Hn & 1)
+    # k_cols: every frame's G in and Q out, plus the state G_{t-1} (the
+    # previous frame's row spectra, F x H) read once per launch (ABI 8; the
+    # state is no longer a 2D spectrum stored and reloaded)
     return {"k_rows_fwd": frames * (W * H * b_in + F * H * 8),
-            "k_cols": frames * (F * H * 8 + F * Hq * 8) + 2 * F * N * 8,
+            "k_cols": frames * (F * H * 8 + F * Hq * 8) + F * H * 8,
             "k_rows_inv": frames * (F * Hq * 8 + Hn * W * 4),
             "k_compose": frames * (Hn * W * 4 + W * H * (b_in + b_out)),
             # K3 + K4 fused (even sizes): Q once, the input for I/Q, the output
@@ -87,7 +95,13 @@ def parse():
                     help="steerable extension's temporal filter (iir: no ring mode)")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: rehearsal of the N>1 path without RCCL (ranks may share one "
-                         "GPU; the ring state goes through host memory)")
+                         "GPU; the ring state goes through host memory; implies --ring-impl torch)")
+    ap.add_argument("--ring-impl", choices=("c", "torch"), default="c",
+                    help="--mode ring transport: c = the C host's RCCL ring (libmm_ring.so, "
+                         "mm_ring_step per step); torch = mm355.ShardedStream over torch.distributed")
+    ap.add_argument("--ring-self", action="store_true",
+                    help="rehearsal at world 1: run the C ring anyway (RCCL send/recv to itself "
+                         "every step)")
     ap.add_argument("--checksum", action="store_true",
                     help="rehearsal: print per-frame output checksums (all ranks, rank 0) "
                          "instead of the bench line; sharded and single-rank runs of the "
@@ -294,8 +308,9 @@ def parity_check(mm355, torch, params, W, H, ref, local):
 def drop_in_per_frame(mm355, torch, params, W, H, frames, local, count):
     """The reference's call pattern (OnRenderImage once per frame,
     .cs:101-143): a fresh handle at batch size 1, mm_process with device
-    pointers, one frame per call on one stream.  Every call pays K2's state
-    load + store and four launches.  Returns frames/s over the calls (after
+    pointers, one frame per call on one stream.  Every call re-transforms the
+    state G_{t-1} (K2's priming column FFT of the previous frame's row
+    spectra) and makes one launch per kernel.  Returns frames/s over the calls (after
     the passthrough frame and 10 warm-up calls) and the HIP-event latency of
     each call."""
     h = mm355.Handle(W, H, params, device=local)
@@ -371,11 +386,14 @@ def main():
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     gloo = a.dist_backend == "gloo"
+    # the C ring carries the data path over its own RCCL communicator; the
+    # process group only exchanges the ring id, the barrier and the max time
+    c_ring = a.mode == "ring" and not gloo and a.ring_impl == "c" and (world > 1 or a.ring_self)
     # gloo rehearsal: ranks may share the box's GPU(s)
     dev = local % torch.cuda.device_count() if gloo else local
     torch.cuda.set_device(dev)
     if world > 1:
-        if gloo:
+        if gloo or c_ring:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
@@ -401,7 +419,7 @@ def main():
 
     # resident inputs: one buffer per step (warmup + timed), generated on device
     total_steps = a.warmup + a.steps
-    ring = a.mode == "ring" and world > 1
+    ring = a.mode == "ring" and world > 1 and not c_ring
     replica = rank if a.replica_index is None else a.replica_index
     seed = 0x5EED0000 + (0 if a.mode == "ring" else replica)
     frames = torch.empty((total_steps, C, H, W, 4), dtype=torch.uint8, device="cuda")
@@ -414,13 +432,30 @@ def main():
     stream = ShardedStream(backend, C, rank if ring else 0, world if ring else 1)
     if a.checksum:
         backend.sums = {}
+    cring = None
+    if c_ring:
+        if per_frame:
+            raise SystemExit("--call-pattern per-frame is a single-GPU measurement")
+        rid = [mm355.new_ring_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(rid, src=0)
+        cring = mm355.Ring(world, rank, rid[0], dev, h, C, mm355.RGBA8)
     torch.cuda.synchronize()
 
     # ring mode overlaps each step's state shift with the previous step's
-    # compute (ShardedStream prefetch); the shift for a step past the end is
-    # never posted
+    # compute (ShardedStream prefetch / mm_ring_step's next_last); the shift
+    # for a step past the end is never posted
     def run_step(s):
-        stream.step(s, prefetch=ring and s + 1 < total_steps)
+        if cring is None:
+            stream.step(s, prefetch=ring and s + 1 < total_steps)
+            return
+        nxt = frames[s + 1, C - 1] if s + 1 < total_steps else None
+        cring.step(s, frames[s], out, nxt, stream=torch.cuda.current_stream().cuda_stream)
+        if backend.sums is not None:
+            v = out.reshape(C, -1).sum(dim=1, dtype=torch.int64).cpu()
+            lo = s * world * C + rank * C
+            for i in range(C):
+                backend.sums[lo + i] = int(v[i])
 
     for s in range(a.warmup):
         run_step(s)
@@ -436,9 +471,11 @@ def main():
     elapsed = time.perf_counter() - t_start
     prof = h.profile_end()
     stream.finish()
+    if cring is not None:
+        cring.close()   # retires shifts posted ahead
     if a.checksum:
         sums = backend.sums
-        if world > 1 and a.mode == "ring":
+        if world > 1 and a.mode == "ring":   # (gloo or nccl process group)
             allv = [None] * world
             dist.all_gather_object(allv, sums)
             sums = {k: v for d in allv for k, v in d.items()}
@@ -461,7 +498,7 @@ def main():
         return
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else "cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo or c_ring else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -518,10 +555,12 @@ def main():
                    "frames_per_step_per_gpu": C, "padded_n": N,
                    "call_pattern": ("one mm_process per frame (batch 1)" if per_frame else
                                     f"mm_process_stream, {C} frames per call in batches of {B}"),
-                   "parallelism": ("single GPU" if world == 1 else
+                   "parallelism": ("single GPU" if world == 1 and not c_ring else
+                                   f"frame-sharded x{world}, C host RCCL ring (libmm_ring "
+                                   f"mm_ring_step, state {h.state_bytes} B per hop)" if c_ring else
                                    f"frame-sharded x{world}, "
                                    + ("gloo rehearsal, ring state via host" if gloo
-                                      else "RCCL ring state shift")
+                                      else "torch.distributed RCCL ring state shift")
                                    if ring else f"replicas x{world}")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",

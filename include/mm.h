@@ -20,7 +20,13 @@
  *   - The first frame after mm_create/mm_reset is passed through bitwise
  *     (alpha included) and becomes the temporal state (.cs:111-117); after
  *     that output alpha is 1 (CombineYIQChannels.shader:56).
- *   - W and H must be even, max(W,H) <= 4096 (padded square N = nextpow2).
+ *   - Geometry: the padded square is N = nextpow2(max(W, H)) (.cs:298-302);
+ *     this build covers 16 <= N <= 4096, i.e. 9 <= max(W, H) <= 4096 (other
+ *     sizes: MM_ERR_UNSUPPORTED from mm_create).  Odd W or H are supported in
+ *     MM_MODE_PYRAMID and MM_MODE_STANDARD (and the debug views);
+ *     MM_MODE_STEERABLE needs even W and H.  The fused K3+K4 kernel runs for
+ *     even sizes with W % 8 == 0 and margins N - W >= 8, N - H >= 4; every
+ *     other geometry takes the unfused pair (same results).
  *   - Every entry point that takes a handle runs on the handle's device and
  *     restores the caller's current HIP device before it returns.
  */
@@ -33,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 7
+#define MM_ABI_VERSION 8   /* 8: the state is G_{t-1} (row spectra), see mm_state_size */
 
 /* error codes */
 #define MM_OK               0
@@ -109,7 +115,9 @@ int mm_params_default(mm_params *p);
 int mm_create(int width, int height, const mm_params *p, int hip_device,
               mm_handle **out);
 
-/* OnValidate (.cs:78-88): new parameters apply from the next frame. */
+/* OnValidate (.cs:78-88): new parameters apply from the next frame.  Does not
+ * synchronise the device: a change of edge_mode (which rewrites the resample
+ * tables) waits only for this handle's own latest work. */
 int mm_set_params(mm_handle *h, const mm_params *p);
 int mm_get_params(const mm_handle *h, mm_params *p);
 
@@ -135,16 +143,19 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count,
 /* isFirstFrame = true (.cs:75): the next frame is passed through. */
 int mm_reset(mm_handle *h);
 
-/* The temporal state carried between frames: the previous frame's spectrum
- * (what previousSourceTexture, .cs:142, is used for).  `dev_buf` is device
- * memory of mm_state_size() bytes.  Ordered on hip_stream (NULL = default stream).
+/* The temporal state carried between frames (previousSourceTexture, .cs:142):
+ * the previous input frame's row half-spectra G_{t-1} (K1's output: complex
+ * fp32 [N/2 + 1][H rounded up to even], rows of the windowed luma after the
+ * stretch+pad resample; 8.86 MB at 1920x1080), from which the next call
+ * recomputes the previous frame's 2D spectrum.  `dev_buf` is device memory of
+ * mm_state_size() bytes.  Ordered on hip_stream (NULL = default stream).
  * MM_MODE_STEERABLE: the per-coefficient local phases (one float plane per
  * band; MM_FILTER_IIR adds the two filter planes), so the size follows the
  * mode, levels, orientations and filter of the current parameters. */
 int mm_state_size(const mm_handle *h, size_t *bytes);
 int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream);
 int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stream);
-/* Compute the state that frame `in` would leave behind (its spectrum) into
+/* Compute the state that frame `in` would leave behind (its row spectra) into
  * dev_buf without touching the handle's own state (used by the multi-GPU ring
  * to hand the chunk-boundary state to the next rank). */
 int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf,
@@ -155,11 +166,13 @@ void *mm_stream(mm_handle *h);
 
 /* Frames per internal batch of mm_process_stream: the launches of one batch
  * cover `frames` frames, and the column kernel keeps the previous spectrum on
- * chip across them (its state is read and written once per batch).  Larger
- * batches amortise that and the launch gaps; the hand-off buffers take about
- * 26 MB per 1080p frame (4x at 2160p).  Default: min(64, 1 GiB of buffers).
- * Results do not depend on the batch size.  Reallocates (synchronises the
- * device); call between frames.  Since ABI 5. */
+ * chip across them (each launch first re-transforms the state G_{t-1}).
+ * Larger batches amortise that and the launch gaps; the hand-off buffers take
+ * about 17.8 MB per 1080p frame (4x at 2160p).  Default: min(64, 2 GiB of
+ * buffers).  Results do not depend on the batch size.  Reallocates
+ * (synchronises the device); call between frames.  Failure-atomic: on
+ * MM_ERR_OOM the handle keeps its previous batch size, buffers and state.
+ * Since ABI 5. */
 int mm_set_batch(mm_handle *h, int frames);
 int mm_get_batch(const mm_handle *h, int *frames);
 

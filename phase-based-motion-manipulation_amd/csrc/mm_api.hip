@@ -45,19 +45,28 @@ struct mm_handle {
     float4 *d_col3, *d_row3;    // the same taps merged onto offsets -1, 0, +1
     c2 *d_tw;
     c2 *d_tw_half;              // W_{N/2} table (debug views, lazily)
-    float *d_dbg;               // debug view textures [chunk][mag, phase][N][N] (lazily)
+    float *d_dbg;               // debug view textures [dbg_frames][mag, phase][N][N] (lazily)
     // MM_MODE_STEERABLE (lazily, for the current levels/orientations):
-    c2 *d_Fb;                   // per chunk frame half spectrum [chunk][N/2+1][N]
+    c2 *d_Fb;                   // per batch frame half spectrum [fb_frames][N/2+1][N] (lazily)
     c2 *d_T;                    // band rows [nb+1][Hq][N] (row-major, k_sb_cols -> k_sb_rows)
     float *d_sst;               // temporal-filter state: phi, u_h, u_l planes [nb][Hn][W+4]
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
     bool steer_valid;           // d_sst holds the state after the previous frame
-    c2 *d_G, *d_Q, *d_state;
-    float *d_Yh;
+    // G: chunk + 1 slots of K1's row spectra.  Slot gs holds G_{t-1}, the row
+    // spectra of the previous input frame: the temporal state
+    // (previousSourceTexture, .cs:142), valid while has_state.  A batch's
+    // frames go to slots that avoid gs (place_batch).
+    c2 *d_G, *d_Q;
+    float *d_Yh;                // unfused K3 -> K4 / steerable rows (lazily, yh_frames)
     size_t g_stride, q_stride, yh_stride;  // elements per frame
     int chunk;                  // frames per K1/K2/K3 batch (mm_set_batch)
+    int gs;                     // G slot of the state
+    int yh_frames, fb_frames, dbg_frames;  // frames the lazy buffers hold
+    hipEvent_t last_ev;         // recorded after this handle's latest work (mm_set_params)
+    bool last_ev_set;
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
+    bool k2_pow;                // ... and the phase factor as z^S (integer S, MM_K2_PYR_POW)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
@@ -90,6 +99,30 @@ struct DeviceScope {
 #define DEVICE_SCOPE(h)                                  \
     DeviceScope dev_scope_((h)->device);                 \
     if (dev_scope_.err != hipSuccess) return MM_ERR_HIP
+
+// hipMalloc that leaves no error behind on failure: a failed allocation sets
+// the thread's last HIP error, which the next launch check (hipGetLastError)
+// would otherwise report as that launch's failure (an OOM from mm_set_batch
+// must leave the handle usable).
+template <class T>
+static hipError_t dev_alloc(T **p, size_t bytes)
+{
+    const hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+    }
+    return e;
+}
+
+// Marks the end of this handle's latest work on stream s (mm_set_params waits
+// for it before rewriting the tables that work may read).
+static int note_work(mm_handle *h, hipStream_t s)
+{
+    HIPCHK(hipEventRecord(h->last_ev, s));
+    h->last_ev_set = true;
+    return MM_OK;
+}
 
 // Brackets one kernel launch with events when profiling is on.
 struct ProfScope {
@@ -190,6 +223,10 @@ static void build_spec(const mm_params &p, int N, Spec &sp)
     sp.tau2 = p.magnitude_threshold * p.magnitude_threshold;
     sp.inv_nn = 1.0f / ((float)N * (float)N);
     sp.S_rev = (float)((double)p.phase_scale / (2.0 * 3.14159265358979323846));
+    // integer phase scale (the reference default 10, BASELINE's 25): the power form
+    const float aS = fabsf(p.phase_scale);
+    sp.S_pow = (aS == floorf(aS) && aS <= 4096.0f) ? (int)aS : -1;
+    sp.S_sgn = p.phase_scale < 0.0f ? -1.0f : 1.0f;
     sp.tau2_nn = sp.tau2 * sp.inv_nn * sp.inv_nn;   // exact: inv_nn is a power of two
     sp.hp_lo = p.max_freq * 0.8f;             // PyramidOperations.compute:36-41
     sp.hp_inv = 1.0f / (p.max_freq * 0.2f);
@@ -296,35 +333,42 @@ static int set_attrs(int W)
 }
 
 template <int LOG2N>
-static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipStream_t s)
+static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipStream_t s, c2 *G)
 {
     const int ppf = (h->H + 1) / 2;   // odd H: the last pair's second row is zero
     const int total = ppf * nframes;
-    const int gpw = k1_groups<LOG2N>();
-    const int blocks = (total + gpw - 1) / gpw;
+    // fewer than 2 workgroups per CU at the batch form: the one-pair form
+    const bool lat = (total + k1_groups<LOG2N>() - 1) / k1_groups<LOG2N>() < 512;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-    const size_t lds = sizeof(c2) * (size_t)gpw * lds_complex<(1 << LOG2N)>();
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
-#define MM_K1_LAUNCH(F, GEN)                                                              \
-    hipLaunchKernelGGL((k_rows_fwd<LOG2N, F, GEN>), dim3(blocks), dim3(k1_threads<LOG2N>()), lds, s, \
-                       in, fb, ppf, total, h->geo, h->d_col3, h->d_row3, h->d_col, h->d_row,       \
-                       h->d_tw, h->d_G, h->g_stride)
+#define MM_K1_LAUNCH(F, GEN, LAT)                                                                  \
+    do {                                                                                           \
+        constexpr int gpw = k1_gpw<LOG2N, LAT>();                                                  \
+        const size_t lds = sizeof(c2) * (size_t)gpw * lds_complex<(1 << LOG2N)>();                \
+        hipLaunchKernelGGL((k_rows_fwd<LOG2N, F, GEN, LAT>), dim3((total + gpw - 1) / gpw),         \
+                           dim3(gpw * fft_T<LOG2N>()), lds, s, in, fb, ppf, total, h->geo,         \
+                           h->d_col3, h->d_row3, h->d_col, h->d_row, h->d_tw, G, h->g_stride);     \
+    } while (0)
     const bool gen = h->geo.ox || h->geo.oy;   // odd W/H: taps span i-2 .. i+1
     if (fmt == MM_RGBA8) {
-        if (gen) MM_K1_LAUNCH(0, true);
-        else MM_K1_LAUNCH(0, false);
+        if (gen) MM_K1_LAUNCH(0, true, false);
+        else if (lat) MM_K1_LAUNCH(0, false, true);
+        else MM_K1_LAUNCH(0, false, false);
     } else {
-        if (gen) MM_K1_LAUNCH(1, true);
-        else MM_K1_LAUNCH(1, false);
+        if (gen) MM_K1_LAUNCH(1, true, false);
+        else if (lat) MM_K1_LAUNCH(1, false, true);
+        else MM_K1_LAUNCH(1, false, false);
     }
 #undef MM_K1_LAUNCH
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
 
+// K2 over frames G[0 .. nframes) (K1's row spectra), primed with Gprev = G_{t-1}
+// (the state slot, or frame 0 itself for a stream's first batch, whose frame 0
+// passes through): Q of frame fr to d_Q + fr * q_stride.
 template <int LOG2N>
-static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 *st_in,
-                     c2 *st_out, hipStream_t s, int g_frame = 0)
+static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hipStream_t s)
 {
     const int gpw = k2_groups<LOG2N>();
     const int cols = (1 << LOG2N) / 2;   // f = 0 and f = N/2 share group 0 (k_cols)
@@ -335,22 +379,64 @@ static int launch_k2(mm_handle *h, int nframes, int first_passthrough, const c2 
     // the packed block's last k frames go to k_cols_tail (k_cols's critical path)
     int k = nframes >= 24 ? nframes * h->k2_tail_pct / 100 : 0;
     k = std::max(0, std::min(k, nframes - 2));
-    const c2 *G0 = h->d_G + h->g_stride * g_frame;
 #define MM_K2_LAUNCH(MODE)                                                                           \
     do {                                                                                             \
-        hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, G0, \
-                           h->g_stride, h->d_Q, h->q_stride, st_in, st_out, nframes, first_passthrough, \
-                           h->geo, h->spec, h->d_tw, nframes - k, k ? nullptr : st_out);           \
+        hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, G, \
+                           h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, \
+                           nframes - k);                                                             \
         if (k)                                                                                       \
-            hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G0, \
-                               h->g_stride, h->d_Q, h->q_stride, st_out, nframes - k, h->geo, h->spec, \
-                               h->d_tw);                                                             \
+            hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G, \
+                               h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw); \
     } while (0)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
+    else if (h->k2_tab && h->k2_pow) MM_K2_LAUNCH(MM_K2_PYR_POW);
     else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB);
     else MM_K2_LAUNCH(MM_MODE_PYRAMID);
 #undef MM_K2_LAUNCH
     HIPCHK(hipGetLastError());
+    return MM_OK;
+}
+
+// Grows a per-batch buffer that only some paths use to `frames` frames of
+// `per_frame` bytes.  Growing waits for the device (in-flight work may still
+// read the old buffer); a failed allocation leaves the old one in place.
+static int ensure_frames(void **buf, int *have, int frames, size_t per_frame)
+{
+    if (*buf && *have >= frames) return MM_OK;
+    void *p = nullptr;
+    if (dev_alloc(&p, per_frame * (size_t)frames) != hipSuccess) return MM_ERR_OOM;
+    if (*buf) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(*buf);
+    }
+    *buf = p;
+    *have = frames;
+    return MM_OK;
+}
+static int ensure_yh(mm_handle *h)
+{
+    return ensure_frames(reinterpret_cast<void **>(&h->d_Yh), &h->yh_frames, h->chunk,
+                         sizeof(float) * h->yh_stride);
+}
+
+// G slot of the first frame of an n-frame batch: the batch must not
+// overwrite the state slot gs (read by the batch's K2 as G_{t-1}).  With
+// chunk + 1 slots the state moves (one slot copy) only when neither the slots
+// after gs nor those before it hold the batch: once per full batch at most,
+// never in the one-frame-per-call pattern (it alternates slots 0 and 1).
+static int place_batch(mm_handle *h, int n, hipStream_t s, int *base)
+{
+    *base = 0;
+    if (!h->has_state) return MM_OK;
+    if (h->gs + 1 + n <= h->chunk + 1) {
+        *base = h->gs + 1;
+        return MM_OK;
+    }
+    if (n > h->gs) {
+        HIPCHK(hipMemcpyAsync(h->d_G + h->g_stride * h->chunk, h->d_G + h->g_stride * h->gs,
+                              sizeof(c2) * h->g_stride, hipMemcpyDeviceToDevice, s));
+        h->gs = h->chunk;
+    }
     return MM_OK;
 }
 
@@ -408,6 +494,8 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     const int ppf = h->geo.Hq / 2;   // whole Q tiles (k_rows_inv)
     const int total = ppf * nout;
     const int gpw = k3_groups<LOG2N>();
+    int rc = ensure_yh(h);
+    if (rc) return rc;
     {
         ProfScope ps(h, s, MM_K_ROWS_INV, nout);
         hipLaunchKernelGGL((k_rows_inv<LOG2N>), dim3((total + gpw - 1) / gpw),
@@ -469,41 +557,47 @@ static size_t steer_state_bytes(const mm_handle *h)
 {
     return sizeof(float) * steer_planes(h) * steer_plane_floats(h);
 }
+// Band buffers and the temporal state planes for the current levels and
+// orientations.  Reallocated (state invalid) only when those change, never
+// by mm_set_batch: the per-batch spectra Fb grow separately (ensure_frames).
 static int steer_alloc(mm_handle *h)
 {
     const int nb = steer_bands(h);
+    const size_t fstride = (size_t)(h->N / 2 + 1) * h->N;
+    int rc = ensure_frames(reinterpret_cast<void **>(&h->d_Fb), &h->fb_frames, h->chunk, sizeof(c2) * fstride);
+    if (rc) return rc;
+    if ((rc = ensure_yh(h))) return rc;
     if (h->steer_nb == nb && h->steer_planes >= steer_planes(h)) return MM_OK;
-    (void)hipFree(h->d_Fb);
+    (void)hipDeviceSynchronize();   // in-flight work may still use the old planes
     (void)hipFree(h->d_T);
     (void)hipFree(h->d_sst);
-    h->d_Fb = h->d_T = nullptr;
+    h->d_T = nullptr;
     h->d_sst = nullptr;
     h->steer_nb = -1;
     h->steer_valid = false;
-    const size_t fstride = (size_t)(h->N / 2 + 1) * h->N;
-    if (hipMalloc(&h->d_Fb, sizeof(c2) * fstride * h->chunk) != hipSuccess ||
-        hipMalloc(&h->d_T, sizeof(c2) * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
-        hipMalloc(&h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
+    if (dev_alloc(&h->d_T, sizeof(c2) * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
+        dev_alloc(&h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
     h->steer_planes = steer_planes(h);
     return MM_OK;
 }
 
-// Chunk frames [0, n): K1 -> k_cols_fwd -> per frame k_sb_cols, k_sb_rows (the
-// temporal filter runs frame by frame) -> K4.  The first `seed` frames (0 or
-// 1: no valid state after create/reset/mode change) pass through and seed it.
-// apply_magnification == false: output passes through, the state keeps
-// following the input.  `sst`: state planes (the handle's or a caller buffer).
+// Batch frames [0, n) with K1's row spectra in G: k_cols_fwd -> per frame
+// k_sb_cols, k_sb_rows (the temporal filter runs frame by frame) -> K4.
+// `sst`: state planes (nullptr: the handle's own, whose first frame passes
+// through and seeds them when they hold no valid state; a caller's buffer
+// (mm_compute_state) is always seeded).  write == false: outputs pass through,
+// the state keeps following the input.
 template <int LOG2N>
 static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int fmt, float *sst,
-                     bool write, int seed, hipStream_t s)
+                     bool write, hipStream_t s, const c2 *G)
 {
     constexpr int N = 1 << LOG2N;
     int rc;
-    if ((rc = steer_alloc(h))) return rc;
+    if ((rc = steer_alloc(h))) return rc;   // may invalidate the handle's planes
+    const int seed = sst ? 1 : (h->steer_valid ? 0 : 1);
     if (!sst) sst = h->d_sst;
-    if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s))) return rc;
     const size_t fstride = (size_t)(N / 2 + 1) * N;
     const int gpw = groups_per_wg<LOG2N>();
     const size_t lds = lds_fft_bytes<LOG2N>();
@@ -511,7 +605,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         const int total = n * (N / 2 + 1);
         ProfScope ps(h, s, MM_K_COLS, n);
         hipLaunchKernelGGL((k_cols_fwd<LOG2N>), dim3((total + gpw - 1) / gpw),
-                           dim3(wg_threads<LOG2N>()), lds, s, h->d_G, h->g_stride, h->d_Fb,
+                           dim3(wg_threads<LOG2N>()), lds, s, G, h->g_stride, h->d_Fb,
                            fstride, total, h->geo, h->d_tw);
         HIPCHK(hipGetLastError());
     }
@@ -537,13 +631,6 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         HIPCHK(hipGetLastError());
     }
     if (sst == h->d_sst) h->steer_valid = true;
-    // the frame spectrum state follows the input in this mode too (.cs:142), so
-    // that a switch back to the pyramid or standard mode magnifies against the
-    // last input: K2 in passthrough on the chunk's last K1 spectrum
-    if (sst == h->d_sst) {
-        if ((rc = launch_k2<LOG2N>(h, 1, 1, nullptr, h->d_state, s, n - 1))) return rc;
-        h->has_state = true;
-    }
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     if (!write) {
         if (out) HIPCHK(hipMemcpyAsync(out, in, fb * n, hipMemcpyDeviceToDevice, s));
@@ -553,89 +640,91 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     return launch_k4(h, in, out, seed, n, fmt, s);
 }
 
-// One batch of `n` consecutive frames (n <= chunk), all on the device.
-// ProcessDebugView (.cs:119-123, :234-257) for chunk frames [first, n): K1's half
-// spectra -> k_dbg_cols (view textures) -> k_dbg_out (crop or split screen);
-// the state then follows the last input frame (.cs:122).
+// ProcessDebugView (.cs:119-123, :234-257) for batch frames [first, n) whose
+// row spectra are in G: k_dbg_cols (view textures) -> k_dbg_out (crop or split
+// screen).  The state follows the input (.cs:122): the caller's slot update.
 template <int LOG2N>
-static int run_debug(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int first, int fmt,
-                     hipStream_t s)
+static int run_debug(mm_handle *h, uint8_t *out, int n, int first, int fmt, hipStream_t s,
+                     const c2 *G)
 {
     constexpr int N = 1 << LOG2N;
-    int rc;
-    if (n > first) {
-        const size_t tex_stride = (size_t)2 * N * N;
-        if (!h->d_dbg) {   // lazily: only handles that show a debug view pay for it
-            HIPCHK(hipMalloc(&h->d_dbg, sizeof(float) * tex_stride * h->chunk));
-            std::vector<c2> twh(N / 2);
-            for (int k = 0; k < N / 2; ++k) {
-                const double a = -2.0 * M_PI * (double)k / (double)(N / 2);
-                twh[k] = mk((float)cos(a), (float)sin(a));
-            }
-            HIPCHK(hipMalloc(&h->d_tw_half, sizeof(c2) * (N / 2)));
-            HIPCHK(hipMemcpy(h->d_tw_half, twh.data(), sizeof(c2) * (N / 2), hipMemcpyHostToDevice));
+    if (n <= first) return MM_OK;
+    const size_t tex_stride = (size_t)2 * N * N;
+    // lazily (only handles that show a debug view pay for it), sized for the batch
+    int rc = ensure_frames(reinterpret_cast<void **>(&h->d_dbg), &h->dbg_frames, h->chunk,
+                           sizeof(float) * tex_stride);
+    if (rc) return rc;
+    if (!h->d_tw_half) {
+        std::vector<c2> twh(N / 2);
+        for (int k = 0; k < N / 2; ++k) {
+            const double a = -2.0 * M_PI * (double)k / (double)(N / 2);
+            twh[k] = mk((float)cos(a), (float)sin(a));
         }
-        if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s))) return rc;
-        const int m = n - first;
-        constexpr int T = fft_T<LOG2N - 1>();
-        hipLaunchKernelGGL((k_dbg_cols<LOG2N>), dim3(m * N), dim3(2 * T),
-                           2 * sizeof(c2) * lds_complex<N / 2>(), s, h->d_G, h->g_stride, h->d_dbg,
-                           tex_stride, first, h->p.show_magnitude, h->p.show_phase, h->geo,
-                           h->d_tw_half);
-        HIPCHK(hipGetLastError());
-        const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-        const size_t tot = (size_t)m * h->W * h->H;
-        const dim3 grid((unsigned)((tot + 255) / 256));
-        if (fmt == MM_RGBA8)
-            hipLaunchKernelGGL((k_dbg_out<0>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
-                               first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
-        else
-            hipLaunchKernelGGL((k_dbg_out<1>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
-                               first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
-        HIPCHK(hipGetLastError());
+        HIPCHK(dev_alloc(&h->d_tw_half, sizeof(c2) * (N / 2)));
+        HIPCHK(hipMemcpy(h->d_tw_half, twh.data(), sizeof(c2) * (N / 2), hipMemcpyHostToDevice));
     }
+    const int m = n - first;
+    constexpr int T = fft_T<LOG2N - 1>();
+    hipLaunchKernelGGL((k_dbg_cols<LOG2N>), dim3(m * N), dim3(2 * T),
+                       2 * sizeof(c2) * lds_complex<N / 2>(), s, G, h->g_stride, h->d_dbg,
+                       tex_stride, first, h->p.show_magnitude, h->p.show_phase, h->geo,
+                       h->d_tw_half);
+    HIPCHK(hipGetLastError());
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-    if ((rc = launch_k1<LOG2N>(h, in + fb * (n - 1), 1, fmt, s))) return rc;
-    if ((rc = launch_k2<LOG2N>(h, 1, 1, nullptr, h->d_state, s))) return rc;
-    h->has_state = true;
+    const size_t tot = (size_t)m * h->W * h->H;
+    const dim3 grid((unsigned)((tot + 255) / 256));
+    if (fmt == MM_RGBA8)
+        hipLaunchKernelGGL((k_dbg_out<0>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
+                           first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
+    else
+        hipLaunchKernelGGL((k_dbg_out<1>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
+                           first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
+    HIPCHK(hipGetLastError());
     return MM_OK;
 }
 
+// One batch of `n` consecutive frames (n <= chunk), all on the device.
 template <int LOG2N>
 static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int fmt,
                      hipStream_t s)
 {
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     const int first = h->has_state ? 0 : 1;
-    int rc;
+    int rc, base;
     if (first) HIPCHK(hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s));
-    if (h->p.show_magnitude || h->p.show_phase) {
-        h->steer_valid = false;   // the debug path does not advance the local-phase state
-        return run_debug<LOG2N>(h, in, out, n, first, fmt, s);
-    }
-    if (h->p.mode == MM_MODE_STEERABLE) {
-        if (first) h->steer_valid = false;
-        rc = run_steer<LOG2N>(h, in, out, n, fmt, nullptr, h->p.apply_magnification != 0,
-                              h->steer_valid ? 0 : 1, s);
-        if (rc == MM_OK) h->has_state = true;
-        return rc;
-    }
-    if (!h->p.apply_magnification) {
+    if ((rc = place_batch(h, n, s, &base))) return rc;
+    c2 *G = h->d_G + h->g_stride * base;
+    // G_{t-1}: the state slot; a stream's first frame primes with itself (its
+    // Q is computed and not used: it passes through)
+    const c2 *Gprev = h->has_state ? h->d_G + h->g_stride * h->gs : G;
+    const bool mag = h->p.apply_magnification != 0;
+    const bool dbg = h->p.show_magnitude || h->p.show_phase;
+    if (!dbg && h->p.mode != MM_MODE_STEERABLE && !mag) {
         // applyMotionMagnification == false: Blit(source, destination) (.cs:139),
-        // but previousSourceTexture still follows the input (.cs:142).
+        // but previousSourceTexture still follows the input (.cs:142): K1 of
+        // the batch's last frame only.
         const int from = first ? 1 : 0;
         if (n > from)
             HIPCHK(hipMemcpyAsync(out + fb * from, in + fb * from, fb * (n - from),
                                   hipMemcpyDeviceToDevice, s));
-        if ((rc = launch_k1<LOG2N>(h, in + fb * (n - 1), 1, fmt, s))) return rc;
-        if ((rc = launch_k2<LOG2N>(h, 1, 1, nullptr, h->d_state, s))) return rc;
+        if ((rc = launch_k1<LOG2N>(h, in + fb * (n - 1), 1, fmt, s, G))) return rc;
+        h->gs = base;
         h->has_state = true;
         return MM_OK;
     }
-    if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s))) return rc;
-    if ((rc = launch_k2<LOG2N>(h, n, first, first ? nullptr : h->d_state, h->d_state, s)))
-        return rc;
-    if ((rc = launch_k3<LOG2N>(h, in, out, first, n, fmt, s))) return rc;
+    if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s, G))) return rc;
+    if (dbg) {
+        h->steer_valid = false;   // the debug path does not advance the local-phase state
+        rc = run_debug<LOG2N>(h, out, n, first, fmt, s, G);
+    } else if (h->p.mode == MM_MODE_STEERABLE) {
+        if (first) h->steer_valid = false;
+        rc = run_steer<LOG2N>(h, in, out, n, fmt, nullptr, mag, s, G);
+    } else {
+        if ((rc = launch_k2<LOG2N>(h, n, Gprev, G, s))) return rc;
+        rc = launch_k3<LOG2N>(h, in, out, first, n, fmt, s);
+    }
+    if (rc) return rc;
+    h->gs = base + n - 1;   // the state follows the input in every mode (.cs:142)
     h->has_state = true;
     return MM_OK;
 }
@@ -653,14 +742,20 @@ static int run_stream(mm_handle *h, const uint8_t *in, uint8_t *out, int count, 
     return MM_OK;
 }
 
+// The state frame `in` leaves behind: its row spectra (K1) straight into dst;
+// steerable DIFF: its local phases (K1 to a free G slot, then the band path).
 template <int LOG2N>
-static int compute_state(mm_handle *h, const uint8_t *in, int fmt, c2 *dst, hipStream_t s)
+static int compute_state(mm_handle *h, const uint8_t *in, int fmt, void *dst, hipStream_t s)
 {
     int rc;
-    if (h->p.mode == MM_MODE_STEERABLE)   // DIFF: the local phases of this frame
-        return run_steer<LOG2N>(h, in, nullptr, 1, fmt, reinterpret_cast<float *>(dst), false, 1, s);
-    if ((rc = launch_k1<LOG2N>(h, in, 1, fmt, s))) return rc;
-    return launch_k2<LOG2N>(h, 1, 1, nullptr, dst, s);
+    if (h->p.mode == MM_MODE_STEERABLE) {
+        int base;
+        if ((rc = place_batch(h, 1, s, &base))) return rc;
+        c2 *G = h->d_G + h->g_stride * base;
+        if ((rc = launch_k1<LOG2N>(h, in, 1, fmt, s, G))) return rc;
+        return run_steer<LOG2N>(h, in, nullptr, 1, fmt, reinterpret_cast<float *>(dst), false, s, G);
+    }
+    return launch_k1<LOG2N>(h, in, 1, fmt, s, reinterpret_cast<c2 *>(dst));
 }
 
 #define MM_DISPATCH(expr_template)                          \
@@ -690,7 +785,7 @@ static int do_stream(mm_handle *h, const uint8_t *in, uint8_t *out, int count, i
     MM_DISPATCH(X)
 #undef X
 }
-static int do_compute_state(mm_handle *h, const uint8_t *in, int fmt, c2 *dst, hipStream_t s)
+static int do_compute_state(mm_handle *h, const uint8_t *in, int fmt, void *dst, hipStream_t s)
 {
 #define X(L) compute_state<L>(h, in, fmt, dst, s)
     MM_DISPATCH(X)
@@ -776,10 +871,10 @@ static void free_handle(mm_handle *h)
     (void)hipFree(h->d_G);
     (void)hipFree(h->d_Q);
     (void)hipFree(h->d_Yh);
-    (void)hipFree(h->d_state);
     (void)hipFree(h->d_stage_in);
     (void)hipFree(h->d_stage_out);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->last_ev) (void)hipEventDestroy(h->last_ev);
     for (auto &r : h->prof_recs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -787,30 +882,45 @@ static void free_handle(mm_handle *h)
     delete h;
 }
 
-// Frames per K1/K2/K3 batch by default: the hand-off buffers of a batch take
-// about 26 MB per 1080p frame; 1 GiB of them keeps K2's per-launch state load
-// and store (one per batch) small against the batch's work.
+// Frames per K1/K2/K3 batch by default: the G and Q hand-off buffers of a
+// batch take 17.8 MB per 1080p frame; 2 GiB of them (of 288 GB) keeps the
+// per-launch costs (K2's priming transform, launch gaps) small against the
+// batch's work.  Yh is not counted: only the unfused, odd-size and steerable
+// paths allocate it (lazily).
 static int default_batch(int W, int H, int N)
 {
-    const size_t per_frame = sizeof(c2) * ((size_t)(N / 2 + 1) * H + (size_t)(N / 2 + 2) * (H + 8)) +
-                             sizeof(float) * (size_t)(H + 4) * W;
-    return (int)std::max<size_t>(1, std::min<size_t>(64, ((size_t)1 << 30) / per_frame));
+    (void)W;
+    const size_t per_frame = sizeof(c2) * ((size_t)(N / 2 + 1) * (H + (H & 1)) + (size_t)(N / 2 + 2) * (H + 8));
+    return (int)std::max<size_t>(1, std::min<size_t>(64, ((size_t)2 << 30) / per_frame));
 }
 
-// (Re)allocates the per-batch hand-off buffers G, Q, Yh for `frames` frames.
+// (Re)allocates the per-batch hand-off buffers G (frames + 1 slots) and Q
+// (frames) for `frames` frames.  Failure-atomic: the new buffers are
+// allocated first and swapped in only when both exist, so on MM_ERR_OOM the
+// handle keeps its old batch and state.  The state slot moves to the new
+// buffer's last slot.  The lazily grown buffers (Yh, Fb, debug views) follow
+// on their next use.
 static int alloc_batch(mm_handle *h, int frames)
 {
+    c2 *G = nullptr, *Q = nullptr;
+    if (dev_alloc(&G, sizeof(c2) * h->g_stride * (size_t)(frames + 1)) != hipSuccess ||
+        dev_alloc(&Q, sizeof(c2) * h->q_stride * (size_t)frames) != hipSuccess) {
+        (void)hipFree(G);
+        return MM_ERR_OOM;
+    }
+    if (h->d_G && h->has_state) {
+        if (hipMemcpy(G + h->g_stride * frames, h->d_G + h->g_stride * h->gs, sizeof(c2) * h->g_stride,
+                      hipMemcpyDeviceToDevice) != hipSuccess) {
+            (void)hipFree(G);
+            (void)hipFree(Q);
+            return MM_ERR_HIP;
+        }
+    }
     (void)hipFree(h->d_G);
     (void)hipFree(h->d_Q);
-    (void)hipFree(h->d_Yh);
-    (void)hipFree(h->d_Fb);   // steerable per-batch spectra: re-sized on next use
-    h->d_G = h->d_Q = h->d_Fb = nullptr;
-    h->d_Yh = nullptr;
-    h->steer_nb = -1;
-    if (hipMalloc(&h->d_G, sizeof(c2) * h->g_stride * frames) != hipSuccess ||
-        hipMalloc(&h->d_Q, sizeof(c2) * h->q_stride * frames) != hipSuccess ||
-        hipMalloc(&h->d_Yh, sizeof(float) * h->yh_stride * frames) != hipSuccess)
-        return MM_ERR_OOM;
+    h->d_G = G;
+    h->d_Q = Q;
+    h->gs = frames;
     h->chunk = frames;
     return MM_OK;
 }
@@ -871,8 +981,12 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     if (((width | height) & 1) && p && p->mode == MM_MODE_STEERABLE) return MM_ERR_UNSUPPORTED;
     int rc = validate_params(p);
     if (rc) return rc;
-    const int N = next_pow2(std::max(std::max(width, height), 16));
-    if (N > 4096) return MM_ERR_UNSUPPORTED;
+    // N = Mathf.NextPowerOfTwo(max(W, H)) (.cs:298-302): the kernels' FFT
+    // layouts cover N = 16 .. 4096, so 2 <= max(W, H) <= 8 (N <= 8) and
+    // 5K / 8K screens (N = 8192) are refused rather than computed on another
+    // canvas than the reference's
+    const int N = next_pow2(std::max(width, height));
+    if (N < 16 || N > 4096) return MM_ERR_UNSUPPORTED;
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MM_ERR_NO_DEVICE;
@@ -910,6 +1024,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.edge = p->edge_mode;
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
+    h->k2_pow = h->spec.S_pow >= 0 && !getenv("MM_K2_NOPOW");
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
@@ -919,17 +1034,17 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->q_stride = (size_t)g.Qs * g.Hq;
     h->yh_stride = (size_t)g.Hq * g.Wy;   // whole Q tiles of rows: K3 stores row pairs
 
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming) != hipSuccess) {
         free_handle(h);
         return MM_ERR_HIP;
     }
-    bool ok = hipMalloc(&h->d_col, sizeof(Tap4) * width) == hipSuccess &&
-              hipMalloc(&h->d_row, sizeof(Tap4) * height) == hipSuccess &&
-              hipMalloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
-              hipMalloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
-              hipMalloc(&h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
-              alloc_batch(h, h->chunk) == MM_OK &&
-              hipMalloc(&h->d_state, sizeof(c2) * (size_t)(N / 2 + 1) * N) == hipSuccess;
+    bool ok = dev_alloc(&h->d_col, sizeof(Tap4) * width) == hipSuccess &&
+              dev_alloc(&h->d_row, sizeof(Tap4) * height) == hipSuccess &&
+              dev_alloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
+              dev_alloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
+              dev_alloc(&h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
+              alloc_batch(h, h->chunk) == MM_OK;
     if (!ok) {
         free_handle(h);
         return MM_ERR_OOM;
@@ -968,7 +1083,10 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     if (p->mode == MM_MODE_STEERABLE && (h->geo.ox || h->geo.oy)) return MM_ERR_UNSUPPORTED;
     const bool edge_changed = p->edge_mode != h->p.edge_mode;
     DEVICE_SCOPE(h);
-    HIPCHK(hipDeviceSynchronize());   // in-flight work on any stream may read the tables
+    // Kernels take the parameters by value at launch, so only a table rewrite
+    // (edge mode) must wait, and only for this handle's own work in flight
+    // (the event recorded after its latest call), never for other streams.
+    if (edge_changed && h->last_ev_set) HIPCHK(hipEventSynchronize(h->last_ev));
     const mm_params &o = h->p;
     if (p->mode != o.mode || p->levels != o.levels || p->orientations != o.orientations ||
         p->temporal_filter != o.temporal_filter || p->min_freq != o.min_freq ||
@@ -979,6 +1097,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
+    h->k2_pow = h->spec.S_pow >= 0 && !getenv("MM_K2_NOPOW");
     if (edge_changed) return upload_tables(h);
     return MM_OK;
 }
@@ -1023,7 +1142,8 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
     if (count == 0) return MM_OK;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
-    return do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
+    const int rc = do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
+    return rc ? rc : note_work(h, s);
 }
 
 int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, void *hip_stream)
@@ -1039,14 +1159,14 @@ int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, v
         (void)hipFree(h->d_stage_out);
         h->d_stage_in = h->d_stage_out = nullptr;
         h->stage_bytes = 0;
-        if (hipMalloc(&h->d_stage_in, fb) != hipSuccess || hipMalloc(&h->d_stage_out, fb) != hipSuccess)
+        if (dev_alloc(&h->d_stage_in, fb) != hipSuccess || dev_alloc(&h->d_stage_out, fb) != hipSuccess)
             return MM_ERR_OOM;
         h->stage_bytes = fb;
     }
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     HIPCHK(hipMemcpyAsync(h->d_stage_in, in, fb, hipMemcpyHostToDevice, s));
     int rc = do_stream(h, h->d_stage_in, h->d_stage_out, 1, format, s);
-    if (rc) return rc;
+    if (rc || (rc = note_work(h, s))) return rc;
     HIPCHK(hipMemcpyAsync(out, h->d_stage_out, fb, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return MM_OK;
@@ -1063,8 +1183,9 @@ int mm_reset(mm_handle *h)
 int mm_state_size(const mm_handle *h, size_t *bytes)
 {
     if (!h || !bytes) return MM_ERR_INVALID;
-    *bytes = h->p.mode == MM_MODE_STEERABLE ? steer_state_bytes(h)
-                                            : sizeof(c2) * (size_t)(h->N / 2 + 1) * h->N;
+    // pyramid / standard: G_{t-1}, K1's half spectra of the previous input
+    // frame's rows ([N/2 + 1][H rounded up to even] complex fp32)
+    *bytes = h->p.mode == MM_MODE_STEERABLE ? steer_state_bytes(h) : sizeof(c2) * h->g_stride;
     return MM_OK;
 }
 
@@ -1078,10 +1199,10 @@ int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
     if (h->p.mode == MM_MODE_STEERABLE) {
         if (!h->steer_valid) return MM_ERR_NO_STATE;
         HIPCHK(hipMemcpyAsync(dev_buf, h->d_sst, need, hipMemcpyDeviceToDevice, s));
-        return MM_OK;
+        return note_work(h, s);
     }
-    HIPCHK(hipMemcpyAsync(dev_buf, h->d_state, need, hipMemcpyDeviceToDevice, s));
-    return MM_OK;
+    HIPCHK(hipMemcpyAsync(dev_buf, h->d_G + h->g_stride * h->gs, need, hipMemcpyDeviceToDevice, s));
+    return note_work(h, s);
 }
 
 int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stream)
@@ -1096,11 +1217,12 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
         HIPCHK(hipMemcpyAsync(h->d_sst, dev_buf, need, hipMemcpyDeviceToDevice, s));
         h->steer_valid = true;
         h->has_state = true;
-        return MM_OK;
+        return note_work(h, s);
     }
-    HIPCHK(hipMemcpyAsync(h->d_state, dev_buf, need, hipMemcpyDeviceToDevice, s));
+    h->gs = h->chunk;   // the spare slot: between calls no batch occupies G
+    HIPCHK(hipMemcpyAsync(h->d_G + h->g_stride * h->gs, dev_buf, need, hipMemcpyDeviceToDevice, s));
     h->has_state = true;
-    return MM_OK;
+    return note_work(h, s);
 }
 
 int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf, size_t bytes,
@@ -1114,7 +1236,8 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
     // the IIR state is a history of frames, not a function of one input frame
     if (h->p.mode == MM_MODE_STEERABLE && h->p.temporal_filter == MM_FILTER_IIR)
         return MM_ERR_UNSUPPORTED;
-    return do_compute_state(h, (const uint8_t *)in_dev, format, (c2 *)dev_buf, s);
+    const int rc = do_compute_state(h, (const uint8_t *)in_dev, format, dev_buf, s);
+    return rc ? rc : note_work(h, s);
 }
 
 void mm_destroy(mm_handle *h)

@@ -53,6 +53,8 @@ struct Spec {
     int L;
     float minF, maxF, S, tau2, inv_nn;
     float S_rev;            // S / (2 pi): phase scale in revolutions (v_sin/v_cos)
+    int S_pow;              // |S| when S is an integer (MM_K2_PYR_POW: e^{i S delta} = z^|S|)
+    float S_sgn;            // sign of S (+1 / -1) for the power form
     float tau2_nn;          // tau2 * inv_nn^2 (gate on masks pre-scaled by inv_nn)
     float hp_lo, hp_inv;    // high-pass ramp start maxF*0.8, 1/(maxF*0.2)
     float lp_hi, lp_inv;    // low-pass ramp end minF*1.2, 1/(minF*0.2)
@@ -97,6 +99,10 @@ template <int LOG2N> constexpr int q_tile() { return q_tile_v(LOG2N); }
 // K1 runs >= 2 row pairs per workgroup so that G receives 32-B pieces
 template <int LOG2N> constexpr int k1_groups() { return groups_at_least<LOG2N, MM_K1_GROUPS>(); }
 template <int LOG2N> constexpr int k1_threads() { return k1_groups<LOG2N>() * fft_T<LOG2N>(); }
+// LAT: short launches (one frame: the drop-in call) run one row pair per
+// workgroup, so that twice as many workgroups spread over the CUs and none
+// waits behind another's latency chain (G then leaves as 16-B pieces)
+template <int LOG2N, bool LAT> constexpr int k1_gpw() { return LAT && fft_T<LOG2N>() >= 64 ? 1 : k1_groups<LOG2N>(); }
 
 __device__ __forceinline__ int wrap_idx(int i, int n, int edge)
 {
@@ -246,15 +252,15 @@ __device__ __forceinline__ float2 chroma_iq(typename Pix<FMT>::raw_t u)
 // =========================================================================
 // GEN (odd W or H): the composite taps of a pixel span i-2 .. i+1 and are
 // read as unmerged Tap4 entries (colT / rowT) instead of the 3-tap tables.
-template <int LOG2N, int FMT, bool GEN = false>
-__global__ __launch_bounds__(k1_threads<LOG2N>())
+template <int LOG2N, int FMT, bool GEN = false, bool LAT = false>
+__global__ __launch_bounds__((k1_gpw<LOG2N, LAT>() * fft_T<LOG2N>()))
 void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pairs_per_frame,
                 int total_pairs, Geo g, const float4 *__restrict__ colW3,
                 const float4 *__restrict__ rowW3, const Tap4 *__restrict__ colT,
                 const Tap4 *__restrict__ rowT, const c2 *__restrict__ tw,
                 c2 *__restrict__ G, size_t g_stride)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k1_groups<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k1_gpw<LOG2N, LAT>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     // group index: wave-uniform (scalar) when a group spans whole waves
     const int grp = GPW == 1 ? 0 : (T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T)
@@ -539,6 +545,17 @@ __device__ __forceinline__ c2 spectral_op(c2 c, c2 p, int fx, int fy, const Spec
 //     The host checks that no 3 bands overlap.
 //   MM_MODE_STANDARD: (w, 0), w = calculate_bandpass_weight (:74-122).
 constexpr int MM_K2_PYR_TAB = 2;
+// MM_K2_PYR_POW: MM_K2_PYR_TAB for an integer phase scale S.  The phase
+// factor of a magnified bin is then a power instead of atan2 + sin/cos:
+//   e^{i S wrap(arg p - arg c)} = e^{i S (arg p - arg c)} = z^S,
+//   z = p conj(c) / (|p| |c|)
+// (wrap subtracts a multiple of 2 pi, which an integer S maps to a multiple
+// of 2 pi: PyramidPhaseDifference.compute:47-54, 92-98).  z^|S| by square and
+// multiply over the bits of |S| (a uniform scalar loop), conj for S < 0.
+// Same value up to fp32 rounding (measured against the oracle's atan2f path:
+// tests/test_k2_pow.py); non-integer S keeps the atan2 form.
+constexpr int MM_K2_PYR_POW = 3;
+template <int MODE> constexpr bool k2_tabled() { return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_POW; }
 
 template <int LOG2N, int MODE>
 __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
@@ -657,6 +674,60 @@ __device__ __forceinline__ c2 pyramid_op_1band(c2 c, c2 p, const Spec &sp, float
     return mul(c, mk(mmag * cw + mpass, mmag * sw));
 }
 
+// pyramid_op_1band in the power form (MM_K2_PYR_POW) for NB bins at once (their
+// squarings interleave): v[j] <- c w, prev[j] <- c for j = j0 .. j0 + NB - 1,
+// w = mpass + mmag z^S, the same gate and masks as pyramid_op_1band.
+template <int NB>
+__device__ __forceinline__ void pyramid_op_pow(c2 (&v)[8], c2 (&prev)[8], int j0, const float2 (&mt)[NB],
+                                               const Spec &sp)
+{
+    c2 z[NB], r[NB];
+    float mmag[NB], mpass[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const c2 c = v[j0 + b], p = prev[j0 + b];
+        const float cn = c.x * c.x + c.y * c.y, pn = p.x * p.x + p.y * p.y;
+        float mn2;   // min without fminf's NaN canonicalisation (finite operands)
+        asm("v_min_f32 %0, %1, %2" : "=v"(mn2) : "v"(cn), "v"(pn));
+        mmag[b] = mt[b].x * mt[b].x * mn2 < sp.tau2_nn ? 0.0f : mt[b].x;
+        mpass[b] = -mt[b].y - mmag[b];
+        // z = u / |u|, |u|^2 = |p|^2 |c|^2 (a zero bin gives z = 0: finite, and
+        // gated there); plain C: the rsq result feeds this multiply
+        const c2 u = mul_conj(p, c);
+        z[b] = u * __builtin_amdgcn_rsqf(fmaxf(cn * pn, 1e-30f));
+    }
+    // r = z^|S|, square and multiply from the lowest set bit (no multiply by
+    // 1): |S| = 25 takes 4 squarings + 2 products, 10 takes 3 + 1.  The bit
+    // loops are uniform (scalar branches only).
+    int e = sp.S_pow;
+    if (e == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) r[b] = mk(1.0f, 0.0f);
+    } else {
+        for (; !(e & 1); e >>= 1) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) z[b] = mul(z[b], z[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) r[b] = z[b];
+        for (e >>= 1; e; e >>= 1) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) z[b] = mul(z[b], z[b]);
+            if (e & 1) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) r[b] = mul(r[b], z[b]);
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const c2 c = v[j0 + b];
+        const c2 w = mk(mmag[b] * r[b].x + mpass[b], (mmag[b] * sp.S_sgn) * r[b].y);
+        prev[j0 + b] = c;
+        v[j0 + b] = mul(c, w);
+    }
+}
+
 template <int MODE>
 __device__ __forceinline__ c2 standard_op_t(c2 c, c2 p, const Spec &sp, float2 mt)
 {
@@ -745,11 +816,15 @@ __device__ unsigned long long mm_k2_stamps[4096 * 8 * 8];
 // packed group, runs the extra exchanges; every other block runs a loop with
 // none of that code, so its register allocation is not shaped by the packed
 // group's live values.
+// The temporal state is G_{t-1}, K1's row spectra of the previous input frame
+// (previousSourceTexture, .cs:142): every launch first runs `Gprev` through
+// the forward transform as a passthrough frame (fr = -1), which sets F_{t-1}
+// in registers bit for bit as the frame loop would have, then frames
+// 0 .. nframes-1 of G, whose Q go to Q + fr * q_stride.
 template <int LOG2N, int MODE, bool BLK0>
-__device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,
-                                            const c2 *state_in, c2 *state_out, int nframes,
-                                            int first_passthrough, const Geo &g, const Spec &sp,
-                                            const c2 *__restrict__ tw, int blk)
+__device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q,
+                                            size_t q_stride, int nframes, const Geo &g,
+                                            const Spec &sp, const c2 *__restrict__ tw, int blk)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     constexpr int TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
@@ -770,12 +845,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     const int f = valid ? f_raw : N / 2 - 1;
     constexpr bool blk0 = BLK0;               // block 0 runs the extra exchanges
     const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
-    c2 *stN = state_out + (size_t)(N / 2) * N;
 
     if constexpr (MODE != MM_MODE_PYRAMID) {
         for (int e = t0; e < TE; e += T) {
             // pyramid table: masks pre-scaled by inv_nn (a power of two: exact)
-            const float ks = MODE == MM_K2_PYR_TAB ? sp.inv_nn : 1.0f;
+            const float ks = k2_tabled<MODE>() ? sp.inv_nn : 1.0f;
             const float2 b0 = bin_static<LOG2N, MODE>(f, e, sp);
             tab0[k2_tix<LOG2N>(e)] = make_float2(b0.x * ks, b0.y * ks);
             if (packed) {
@@ -791,7 +865,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     // packed group: bin j's op column (0 or N/2) and bin within it
     auto pk_col0 = [&](int j, int fy) { return j < 4 || fy == N / 2; };
     bool wave_two_band = true;
-    if constexpr (MODE == MM_K2_PYR_TAB) {
+    if constexpr (k2_tabled<MODE>()) {
         bool two = false;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -803,16 +877,23 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             two |= !__builtin_signbit(tabN[k2_tix<LOG2N>(0)].y) || !__builtin_signbit(tabN[k2_tix<LOG2N>(N / 2)].y);
         wave_two_band = __any(two);
     }
+    // F_{t-1}: set by the passthrough frame fr = -1 (Gprev)
     c2 prev[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int fy = fft_bin<LOG2N>(t0, j);
-        const size_t at = packed && !pk_col0(j, fy) ? (size_t)(N / 2) * N + (N - fy) : (size_t)f * N + fy;
-        prev[j] = state_in ? state_in[at] : mk(0.0f, 0.0f);
-    }
-    if (packed && t0 == 0) {   // FN(0), FN(N/2) of F_{t-1} (read after the loop's barriers)
-        ldsX[0] = state_in ? state_in[(size_t)(N / 2) * N] : mk(0.0f, 0.0f);
-        ldsX[1] = state_in ? state_in[(size_t)(N / 2) * N + N / 2] : mk(0.0f, 0.0f);
+    for (int j = 0; j < 8; ++j) prev[j] = mk(0.0f, 0.0f);
+    // per-bin table bases of a regular group's bins (regular_op): bin j is
+    // fy = fy0 + j N/8 (fy0 = fft_bin(t, 0)), table entry fy for j < 4, N - fy
+    // for j >= 4; N/8 is a multiple of C, so both are slots of two
+    // frame-invariant bases plus immediates (k2_tix): entry fy0 + m C at slot
+    // k2_tix(fy0) + m, entry M - fy0 (M a multiple of C) at slot
+    // k2_tix(C - w) - 1 - fy0 / C + M / C for w = fy0 mod C > 0.
+    const float2 *tlo0, *thi0;
+    {
+        constexpr int C = fft_c_v(LOG2N);
+        const int fy0 = fft_bin<LOG2N>(t0, 0);
+        const int w = fy0 % C;
+        tlo0 = tab0 + k2_tix<LOG2N>(fy0);
+        thi0 = tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
     }
 
     // G column of a frame.  Rows outside the image get an out-of-range buffer
@@ -829,8 +910,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     // at byte offset (t - y0) 8 + j T 8, and rows outside the image (negative
     // offsets wrap to huge ones) fail the range check without any compare.
     auto load_g = [&](int fr, int t) {
-        const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform
-        const c2 *Gc = G + (size_t)gfr * g_stride;
+        const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform; -1: Gprev
+        const c2 *Gc = gfr < 0 ? Gprev : G + (size_t)gfr * g_stride;
         const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)f * g.Hg, 0,
                                                            g.H * (int)sizeof(c2), 0x00020000);
         const unsigned o0 = (unsigned)(t - g.y0) * 8u;
@@ -856,8 +937,27 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     constexpr int TK = q_tile<LOG2N>(), BLK = GPW * TK / 2;   // float4 per tile row
     constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
     const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
-    c2 *stg = lds_all;   // staged Q pieces of a frame: [Hq/TK][GPW][TK]
+    c2 *stg = lds_all;   // staged Q pieces of a frame: [row pair][GPW][TK]
     bool staged = false;   // stg holds the previous frame's pieces (uniform)
+    // Canvas-row staging (TK == 2, rb even, no list row wrapping: every
+    // geometry but H close to N): the inverse transform's rows n = t + jT go
+    // to LDS unconditionally at slot(n) = ((n/2) GPW + grp) TK + n%2 (one base
+    // + immediates, no per-row checks), and the Q stores read list row pair kt
+    // at canvas pair kt + rb/2.  Otherwise list-row staging (rows of [0, Hq)).
+    const bool cstage = TK == 2 && (g.rb & 1) == 0 && g.rb >= 0 && g.rb + g.Hq <= N;
+    const int rd_off = cstage ? (g.rb / 2) * GPW : 0;   // float4 pieces
+    // frame-invariant per-thread Q store offsets (loop invariant: computed
+    // from t0, not the opaque t below); a frame with nothing staged stores
+    // through an empty buffer range instead
+    unsigned so_st[NST];
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+        const int e = grp * T + t0 + i * GPW * T;
+        const int kt = e / BLK, r = e - kt * BLK;
+        const bool ok = e < nq && (GPW <= N / 2 || fb + (2 * r) / TK < N / 2);   // tiny N: fewer columns than groups
+        so_st[i] = ok ? (unsigned)((kt * g.Qs + fb) * TK + 2 * r) * 8u : 0x80000000u;
+    }
+    const float4 *rd_base = reinterpret_cast<const float4 *>(stg) + grp * T + t0 + rd_off;
 
     // One straight path per iteration: G loads of frame fr, then the Q stores
     // of frame fr-1 from the staging buffer (exactly NST buffer stores per
@@ -869,7 +969,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
     st_acc[7] = __builtin_amdgcn_s_memrealtime();   // loop start (100 MHz, device-wide)
 #endif
-    for (int fr = 0;; ++fr) {
+    for (int fr = -1;; ++fr) {
         // Opaque per-iteration copy of the lane index: stops LICM from hoisting
         // every t-derived LDS address and twiddle of both FFTs out of the frame
         // loop (that pinned ~200 VGPRs and capped occupancy at 1 wave/SIMD).
@@ -892,26 +992,18 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         __builtin_amdgcn_sched_barrier(0);   // keep the stores behind the loads
         {
             float4 sv[NST];
-            unsigned so[NST];
 #pragma unroll
-            for (int i = 0; i < NST; ++i) {
-                const int e = grp * T + t + i * GPW * T;   // opaque t: not hoisted
-                const int kt = e / BLK, r = e - kt * BLK;
-                const bool ok = staged && e < nq &&
-                                (GPW <= N / 2 || fb + (2 * r) / TK < N / 2);   // tiny N: fewer columns than groups
-                sv[i] = reinterpret_cast<const float4 *>(stg)[ok ? e : 0];
-                so[i] = ok ? (unsigned)((kt * g.Qs + fb) * TK + 2 * r) * 8u : 0x80000000u;
-            }
+            for (int i = 0; i < NST; ++i) sv[i] = rd_base[i * GPW * T];   // (slots past the staging: unused)
             __syncthreads();   // staging read before this frame's FFT rewrites the buffers
             const int qfr = __builtin_amdgcn_readfirstlane(fr > 0 ? fr - 1 : 0);   // uniform
             const auto qrs = __builtin_amdgcn_make_buffer_rsrc(
-                Q + (size_t)qfr * q_stride, 0, (int)(q_stride * sizeof(c2)), 0x00020000);
+                Q + (size_t)qfr * q_stride, 0, staged ? (int)(q_stride * sizeof(c2)) : 0, 0x00020000);
 #pragma unroll
             for (int i = 0; i < NST; ++i) {
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                 const u32x4 d = {__float_as_uint(sv[i].x), __float_as_uint(sv[i].y),
                                  __float_as_uint(sv[i].z), __float_as_uint(sv[i].w)};
-                __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so[i], 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so_st[i], 0, 0);
             }
             // column N/2 of frame fr-1 (block 0 only).  Read after the barrier:
             // stgN is rewritten only after the packed section's first barrier below.
@@ -920,7 +1012,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
             for (int i = 0; i < NSTN; ++i) {
                 const int e = grp * T + t + i * GPW * T;
                 const bool ok = staged && e < g.Hq / 2;   // rows 2e, 2e+1 (one tile: TK even)
-                const float2 p = reinterpret_cast<const float2 *>(stgN)[ok ? e : 0];
+                const float2 p = reinterpret_cast<const float2 *>(stgN)[ok ? e + (cstage ? g.rb / 2 : 0) : 0];
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                 const u32x4 d = {__float_as_uint(p.x), 0u, __float_as_uint(p.y), 0u};
                 __builtin_amdgcn_raw_buffer_store_b128(
@@ -946,12 +1038,30 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         fft_dif<LOG2N, -1>(v, t, lds, wt);
         MM_MARK("M2_fwd_end");
         K2_STAMP(3);
-        const bool pass_frame = fr == 0 && first_passthrough;
+        const bool pass_frame = fr < 0;
         // the spectral op of a regular group (all groups but the packed one)
         auto regular_op = [&]() {
             if (pass_frame) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) prev[j] = v[j];
+            } else if (MODE == MM_K2_PYR_POW && !wave_two_band) {
+                // integer phase scale: the power form, two bins at a time (the
+                // table addressing of the branch above)
+                constexpr int C = fft_c_v(LOG2N);
+                const float2 *tlo = tlo0, *thi = thi0;   // (frame-invariant: hoisted)
+#ifndef MM_K2_POWG
+#define MM_K2_POWG 4   // bins per power loop (its scalar control and phi moves amortise over them; 8 spills)
+#endif
+#pragma unroll
+                for (int j = 0; j < 8; j += MM_K2_POWG) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    float2 mt[MM_K2_POWG];
+#pragma unroll
+                    for (int b = 0; b < MM_K2_POWG; ++b)
+                        mt[b] = j + b < 4 ? tlo[(j + b) * (N / 8) / C] : thi[(N - (j + b) * (N / 8)) / C];
+                    pyramid_op_pow<MM_K2_POWG>(v, prev, j, mt, sp);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
                 // no bin of this wave has two middle bands: branch-free op, bins
                 // interleaved MM_K2_OPG at a time
@@ -962,10 +1072,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                 // k2_tix(fy0) + m, entry M - fy0 (M a multiple of C) at slot
                 // k2_tix(C - w) - 1 - fy0 / C + M / C for w = fy0 mod C > 0.
                 constexpr int C = fft_c_v(LOG2N);
-                const int fy0 = fft_bin<LOG2N>(t, 0);
-                const int w = fy0 % C;
-                const float2 *tlo = tab0 + k2_tix<LOG2N>(fy0);
-                const float2 *thi = tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
+                const float2 *tlo = tlo0, *thi = thi0;   // (frame-invariant: hoisted)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
@@ -1008,7 +1115,16 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
                     v[j] = pk_col0(j, fy) ? f0 : mk(fn.x, -fn.y);                // or FN(N - fy)
                 }
                 if (!pass_frame) {
-                    if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
+                    if (MODE == MM_K2_PYR_POW && !wave_two_band) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
+                            const int fy = fft_bin<LOG2N>(t, j);
+                            const float2 mt[1] = {pk_col0(j, fy) ? tab0[k2_tix<LOG2N>(fy)]
+                                                                 : tabN[k2_tix<LOG2N>(N - fy)]};
+                            pyramid_op_pow<1>(v, prev, j, mt, sp);
+                        }
+                    } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
@@ -1102,7 +1218,16 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
         // Rows that never wrap (rb >= 0, rb + Hq <= N, every geometry but H
         // close to N): list row k = t + jT - rb, staging slot s(k) = s(k0) + jT GPW
         // (T a multiple of TK): one base and immediate offsets.
-        if (T % TK == 0 && g.rb >= 0 && g.rb + g.Hq <= N) {
+        if (cstage) {
+            const int s0 = ((t >> 1) * GPW + grp) * TK + (t & 1);   // T even: (t + jT)/2 = t/2 + jT/2
+            if (valid) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    stg[s0 + j * (T / 2) * GPW * TK] = packed ? mk(v[j].x, 0.0f) : v[j];
+                    if (packed) stgN[t + j * T] = v[j].y;
+                }
+            }
+        } else if (T % TK == 0 && g.rb >= 0 && g.rb + g.Hq <= N) {
             const int k0 = t - g.rb;   // may be negative: floor division below
             const int s0 = ((k0 >> ilog2c(TK)) * GPW) * TK + (k0 & (TK - 1));
 #pragma unroll
@@ -1139,38 +1264,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
     st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
     if (threadIdx.x % 64 == 0) {
         // k_cols_tail's workgroups (one per frame) after k_cols's 4096 waves
-        const int w = (blk0 && nframes == 2 && first_passthrough && gridDim.x < 512 ? 4096 : 0) +
+        const int w = (blk0 && nframes == 1 && gridDim.x < 512 ? 4096 : 0) +
                       blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
         for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
     }
 #endif
-    if (valid && state_out) {   // (k_cols_tail: only the last frame's workgroup)
-        if (packed) {
-            // column 0 from bins fy <= N/2 (j < 4, and N/2 at thread 0), column
-            // N/2 from bins N - fy (j >= 4) and thread 0's two real bins; the
-            // other halves are the Hermitian mirrors (bitwise: the unpack gives
-            // F[N-fy] = conj F[fy]).
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int fy = fft_bin<LOG2N>(t0, j);
-                const c2 p = prev[j], pc = mk(p.x, -p.y);
-                if (pk_col0(j, fy)) {
-                    state_out[fy] = p;
-                    if (fy != 0 && fy != N / 2) state_out[N - fy] = pc;
-                } else {
-                    stN[N - fy] = p;
-                    stN[fy] = pc;
-                }
-            }
-            if (t0 == 0) {
-                stN[0] = ldsX[0];
-                stN[N / 2] = ldsX[1];
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) state_out[(size_t)f * N + fft_bin<LOG2N>(t0, j)] = prev[j];
-        }
-    }
 }
 
 #ifndef MM_K2_WAVES
@@ -1179,40 +1277,35 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, c2 *Q,
 
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
-void k_cols(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
-            const c2 *state_in, c2 *state_out, int nframes, int first_passthrough,
-            Geo g, Spec sp, const c2 *__restrict__ tw, int nframes_blk0, c2 *state_out_blk0)
+void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
+            int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, int nframes_blk0)
 {
     // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
     // are merged in one L2 (split over XCDs they left as partial-line writes)
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     if (blk == 0)   // the packed block stops nframes_blk0 frames in (k_cols_tail)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Q, q_stride, state_in, state_out_blk0, nframes_blk0,
-                                       first_passthrough, g, sp, tw, blk);
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, blk);
     else
-        k_cols_body<LOG2N, MODE, false>(G, g_stride, Q, q_stride, state_in, state_out, nframes,
-                                        first_passthrough, g, sp, tw, blk);
+        k_cols_body<LOG2N, MODE, false>(G, g_stride, Gprev, Q, q_stride, nframes, g, sp, tw, blk);
 }
 
-// The packed block's last k frames, one workgroup per frame, after k_cols.
+// The packed block's last frames, one workgroup per frame, after k_cols.
 // Block 0 carries the packed group's extra exchanges and is k_cols's critical
 // path, so the other blocks would idle at the end of the launch (rocprofv3:
 // k_cols 1,016 us per 100 frames alone; 939 us + 24.5 us of k_cols_tail with
 // the last 30 frames moved, 940 + 24.6 with 45: the 30 % default is past the
-// point where block 0 stops being the critical path).  The state is a
-// pure function of the previous input frame (.cs:142), so workgroup i starts
-// from frame f0 + i - 1 as a passthrough frame (its forward FFT sets F_{t-1}
-// exactly as the frame loop would: bitwise the same outputs) and then runs
-// frame f0 + i.  The last one writes the columns' state.
+// point where block 0 stops being the critical path).  The state is a pure
+// function of the previous input frame (.cs:142), so workgroup i primes with
+// frame f0 + i - 1 (its passthrough frame sets F_{t-1} exactly as the frame
+// loop would: bitwise the same outputs) and then runs frame f0 + i.
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
-void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, c2 *state_out, int f0,
-                 Geo g, Spec sp, const c2 *__restrict__ tw)
+void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, int f0, Geo g, Spec sp,
+                 const c2 *__restrict__ tw)
 {
     const int fr = f0 + (int)blockIdx.x;   // >= 1
-    k_cols_body<LOG2N, MODE, true>(G + (size_t)(fr - 1) * g_stride, g_stride, Q + (size_t)(fr - 1) * q_stride,
-                                   q_stride, nullptr, blockIdx.x + 1 == gridDim.x ? state_out : nullptr, 2, 1,
-                                   g, sp, tw, 0);
+    k_cols_body<LOG2N, MODE, true>(G + (size_t)fr * g_stride, g_stride, G + (size_t)(fr - 1) * g_stride,
+                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, 0);
 }
 
 // =========================================================================

@@ -198,6 +198,13 @@ int main(int argc, char **argv)
     p.mode = standard ? MM_MODE_STANDARD : MM_MODE_PYRAMID;
     p.show_magnitude = show_mag;
     p.show_phase = show_phase;
+    /* mm_create runs on `dev` and gives the caller's current device back:
+     * this program's own buffers, events and default stream must be on `dev`
+     * too (before its first HIP allocation) */
+    if (hipSetDevice(dev) != hipSuccess) {
+        fprintf(stderr, "hipSetDevice(%d) failed\n", dev);
+        return 1;
+    }
     mm_handle *h = NULL;
     CHECK(mm_create(W, H, &p, dev, &h));
     int N = 0;

@@ -22,9 +22,10 @@ from .binding import (MMError, lib, load_library, LIB_PATH, RGBA8, RGBA32F,
                       abi_symbols, resample_table, strerror)
 from .processor import MotionMagnificationProcessor
 from .stream import ShardedStream, shard_range
+from .ring import Ring, new_ring_id, ring_lib
 
 __all__ = ["MMError", "lib", "load_library", "LIB_PATH", "RGBA8", "RGBA32F",
            "EDGE_REPEAT", "EDGE_CLAMP", "MODE_PYRAMID", "MODE_STANDARD", "MODE_STEERABLE",
            "FILTER_DIFF", "FILTER_IIR", "Params", "Handle", "abi_symbols",
            "resample_table", "strerror", "MotionMagnificationProcessor",
-           "ShardedStream", "shard_range"]
+           "ShardedStream", "shard_range", "Ring", "new_ring_id", "ring_lib"]

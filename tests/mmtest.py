@@ -91,3 +91,29 @@ def assert_close_u8(gpu, ref):
     d = np.abs(gpu.astype(np.int32) - ref.astype(np.int32))
     assert d.max() <= 1, d.max()
     assert (d > 0).mean() <= U8_FRAC, (d > 0).mean()
+
+
+def state_rows(st, N, H):
+    """The pyramid/standard state (mm_get_state / mm_compute_state, ABI 8):
+    G_{t-1}[f][r], complex fp32, f = 0..N/2, r = 0..H-1 (rows rounded up to
+    even in the buffer) -> complex128 [N/2+1][H]."""
+    Hg = H + (H & 1)
+    a = st.view(np.float32) if isinstance(st, np.ndarray) else st.view(dtype=__import__("torch").float32).cpu().numpy()
+    a = a.reshape(N // 2 + 1, Hg, 2).astype(np.float64)
+    return (a[..., 0] + 1j * a[..., 1])[:, :H]
+
+
+def spectrum_from_state(G, N, H):
+    """2D half spectrum [fx = 0..N/2][fy = 0..N) (unshifted) of the canvas the
+    state's rows sit in (image rows at y0 = (N - H) // 2, zero elsewhere)."""
+    y0 = (N - H) // 2
+    col = np.zeros((G.shape[0], N), np.complex128)
+    col[:, y0:y0 + H] = G
+    return np.fft.fft(col, axis=1)
+
+
+def centered_to_half(Fc, N):
+    """Oracle's fftshift-ed 2D spectrum Fc[y][x] -> [fx = 0..N/2][fy = 0..N)."""
+    fx = np.arange(N // 2 + 1)
+    fy = np.arange(N)
+    return Fc[((fy + N // 2) % N)[None, :], ((fx + N // 2) % N)[:, None]]

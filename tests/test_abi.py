@@ -22,7 +22,7 @@ def test_library_loads_and_exports_header_symbols():
     assert not missing, missing
     for s in syms:
         assert hasattr(L, s)
-    assert L.mm_abi_version() == 7
+    assert L.mm_abi_version() == 8
 
 
 def test_strerror_and_defaults():
@@ -41,6 +41,10 @@ def test_create_rejects_bad_arguments_without_gpu():
     st = mm355.Params.make(mode=mm355.MODE_STEERABLE, orientations=8)
     assert L.mm_create(63, 48, ctypes.byref(st), 0, ctypes.byref(h)) == -2  # odd width: steerable only
     assert L.mm_create(8192, 48, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N > 4096
+    assert L.mm_create(4097, 2160, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N = 8192 (5K)
+    assert L.mm_create(8, 6, ctypes.byref(p), 0, ctypes.byref(h)) == -2      # N = 8 < 16
+    assert L.mm_create(2, 2, ctypes.byref(p), 0, ctypes.byref(h)) == -2      # N = 2
+    assert not h.value                                                       # nothing created
     bad = mm355.Params.make()
     bad.orientations = 8
     assert L.mm_create(64, 48, ctypes.byref(bad), 0, ctypes.byref(h)) == -2

@@ -100,7 +100,7 @@ def test_mode_switch_steerable_to_pyramid():
     out = torch.empty_like(dev)
     h.process_stream(dev[:3], out[:3], 3, mm355.RGBA32F)
     h.set_params(pyr)
-    assert h.state_bytes == (h.N // 2 + 1) * h.N * 8   # follows the mode
+    assert h.state_bytes == (h.N // 2 + 1) * (H + (H & 1)) * 8   # follows the mode (G, ABI 8)
     h.process_stream(dev[3:], out[3:], n - 3, mm355.RGBA32F)
     ref = mm355.Handle(W, H, pyr)
     st = torch.empty(ref.state_bytes, dtype=torch.uint8, device="cuda")
@@ -161,11 +161,12 @@ def _bench_checksums(args, world):
 
 
 def test_bench_replicas_gloo_world2():
-    """C5 rehearsal: bench.py --mode replicas at world 2 (gloo, both ranks on
-    this GPU): rank r runs its own stream (seed base + r); each rank's
-    per-frame output checksums equal a single-rank run of that stream."""
+    """C5 rehearsal at its workload size, 1920x1080: bench.py --mode replicas
+    at world 2 (gloo, both ranks on this GPU): rank r runs its own stream (seed
+    base + r); each rank's per-frame output checksums equal a single-rank run
+    of that stream."""
     common = ["--mode", "replicas", "--dist-backend", "gloo", "--checksum", "--steps", "2",
-              "--warmup", "1", "--frames-per-step", "6", "--width", "320", "--height", "240"]
+              "--warmup", "1", "--frames-per-step", "6", "--width", "1920", "--height", "1080"]
     both = _bench_checksums(common + ["--gpus", "2"], 2)["checksums_by_rank"]
     for r in (0, 1):
         one = _bench_checksums(common + ["--gpus", "1", "--replica-index", str(r)], 1)

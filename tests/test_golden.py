@@ -90,9 +90,9 @@ def test_gpu_spectrum_matches_golden():
     st = torch.empty(h.state_bytes, dtype=torch.uint8, device="cuda")
     h.compute_state(torch.from_numpy(inputs_f32(case)[1]).cuda(), mm355.RGBA32F, st)
     torch.cuda.synchronize()
-    half = st.view(torch.float32).cpu().numpy().reshape(N // 2 + 1, N, 2)
-    half = half[..., 0] + 1j * half[..., 1]
-    fx, fy = np.arange(N // 2 + 1), np.arange(N)
-    ref = F[((fy + N // 2) % N)[None, :], ((fx + N // 2) % N)[:, None]]
+    import mmtest as T
+    H = c["height"]
+    half = T.spectrum_from_state(T.state_rows(st, N, H), N, H)   # the state is G (ABI 8)
+    ref = T.centered_to_half(F, N)
     assert np.abs(half - ref).max() / np.abs(ref).max() < 2e-6
     h.close()

@@ -74,7 +74,9 @@ def test_apply_off_passthrough_and_state():
 
 
 def test_forward_spectrum_matches_oracle():
-    """K1+K2 forward path alone: mm_compute_state vs the oracle's F_t."""
+    """K1's forward path alone: mm_compute_state (the state G_t, row half
+    spectra) vs the oracle's windowed luma rows (rfft) and, transformed over
+    the padded columns, vs the oracle's 2D spectrum F_t."""
     import torch
     import mm355
     W, H = 128, 96
@@ -82,18 +84,18 @@ def test_forward_spectrum_matches_oracle():
     o = O.Oracle(W, H)
     o.process(f0)
     _, dbg = o.process(f1, dbg=True)
-    Fc = dbg["F_cur"]
     h = mm355.Handle(W, H)
     N = h.N
+    assert h.state_bytes == (N // 2 + 1) * H * 8
     st = torch.empty(h.state_bytes, dtype=torch.uint8, device="cuda")
     h.compute_state(torch.from_numpy(f1).cuda(), mm355.RGBA32F, st)
     torch.cuda.synchronize()
-    half = st.view(torch.float32).cpu().numpy().reshape(N // 2 + 1, N, 2)
-    half = half[..., 0] + 1j * half[..., 1]
-    fx = np.arange(N // 2 + 1)
-    fy = np.arange(N)
-    ref = Fc[((fy + N // 2) % N)[None, :], ((fx + N // 2) % N)[:, None]]
-    assert np.abs(half - ref).max() / np.abs(ref).max() < 2e-6
+    G = T.state_rows(st, N, H)
+    y0 = (N - H) // 2
+    rows = np.fft.rfft(dbg["y_cur"][y0:y0 + H].astype(np.float64), axis=1).T
+    assert np.abs(G - rows).max() / np.abs(rows).max() < 2e-6
+    ref = T.centered_to_half(dbg["F_cur"], N)
+    assert np.abs(T.spectrum_from_state(G, N, H) - ref).max() / np.abs(ref).max() < 2e-6
     h.close()
 
 

@@ -1,0 +1,259 @@
+"""Handle lifecycle on the HIP path (through the C-ABI): batch changes,
+allocation failure, the G_{t-1} state slots, parameter changes that must not
+stall other handles, and the geometries at the edges of the build.
+
+Every comparison is bitwise against an untouched handle or an uninterrupted
+stream (the results do not depend on the batch size, include/mm.h), or
+against the oracle at the SURVEY.md §8c bars.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import mmtest as T
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(frames):
+    import torch
+    return torch.from_numpy(np.stack(frames)).cuda()
+
+
+def _stream(h, dev, fmt, chunks):
+    """Process dev[0..n) through h in calls of the given frame counts."""
+    import torch
+    out = torch.empty_like(dev)
+    k = 0
+    for c in chunks:
+        h.process_stream(dev[k:k + c], out[k:k + c], c, fmt)
+        k += c
+    torch.cuda.synchronize()
+    return out
+
+
+def test_set_batch_oom_keeps_handle_intact():
+    """mm_set_batch failure-atomic: with most of the device
+    memory taken, a 4096-frame batch at 1080p gets its G buffer but not its Q
+    buffer; mm_set_batch returns MM_ERR_OOM and the handle keeps its batch,
+    buffers and state: frames after the failure equal an untouched handle's."""
+    import torch
+    import mm355
+    W, H = 1920, 1080
+    fr = T.synth(W, H, 6, fmt="u8")
+    dev = _dev(fr)
+    p = mm355.Params.make(phase_scale=25.0)
+    a, b = mm355.Handle(W, H, p), mm355.Handle(W, H, p)
+    a.set_batch(4), b.set_batch(4)
+    oa, ob = torch.empty_like(dev), torch.empty_like(dev)
+    a.process_stream(dev[:3], oa[:3], 3, mm355.RGBA8)
+    b.process_stream(dev[:3], ob[:3], 3, mm355.RGBA8)
+    torch.cuda.synchronize()
+    free, _ = torch.cuda.mem_get_info()
+    g_bytes = 4097 * (1024 + 1) * 1080 * 8          # G: 36 GB, Q: 36 GB
+    filler = None
+    leave = g_bytes + (8 << 30)                       # room for G, not for G + Q
+    if free > leave:
+        filler = torch.empty(free - leave, dtype=torch.uint8, device="cuda")
+    with pytest.raises(mm355.MMError) as ei:
+        a.set_batch(4096)
+    assert ei.value.code == -5                        # MM_ERR_OOM
+    del filler
+    torch.cuda.empty_cache()
+    assert a.batch == 4
+    a.process_stream(dev[3:], oa[3:], 3, mm355.RGBA8)
+    b.process_stream(dev[3:], ob[3:], 3, mm355.RGBA8)
+    torch.cuda.synchronize()
+    assert torch.equal(oa, ob)
+    a.close(), b.close()
+
+
+def test_default_batch_without_yh_and_results_batch_independent():
+    """The fused path allocates no Yh: the default batch at
+    1080p is 64 (2 GiB of G + Q), and a default-batch stream equals a batch-5
+    stream bitwise."""
+    import mm355
+    W, H = 1920, 1080
+    h = mm355.Handle(W, H, mm355.Params.make(phase_scale=25.0))
+    assert h.batch == 64
+    fr = T.synth(W, H, 12, fmt="u8")
+    dev = _dev(fr)
+    a = _stream(h, dev, mm355.RGBA8, [12])
+    h2 = mm355.Handle(W, H, mm355.Params.make(phase_scale=25.0))
+    h2.set_batch(5)
+    b = _stream(h2, dev, mm355.RGBA8, [12])
+    import torch
+    assert torch.equal(a, b)
+    h.close(), h2.close()
+
+
+@pytest.mark.parametrize("batch,chunks", [(1, [1] * 9), (3, [2, 1, 4, 2]), (4, [9]), (8, [5, 4])])
+def test_state_slots_any_call_pattern(batch, chunks):
+    """G_{t-1} slot placement (place_batch): every mix of call sizes and batch
+    sizes, including the one-frame-per-call pattern (slots alternate) and the
+    slot copy, gives the uninterrupted single-call stream bitwise."""
+    import mm355
+    W, H = 200, 120
+    fr = T.synth(W, H, 9)
+    dev = _dev(fr)
+    p = mm355.Params.make(phase_scale=25.0)
+    ref_h = mm355.Handle(W, H, p)
+    ref_h.set_batch(9)
+    ref = _stream(ref_h, dev, mm355.RGBA32F, [9])
+    h = mm355.Handle(W, H, p)
+    h.set_batch(batch)
+    got = _stream(h, dev, mm355.RGBA32F, chunks)
+    import torch
+    assert torch.equal(got, ref)
+    ora = T.oracle_run(W, H, fr, 5, 25.0)
+    for k in range(1, 9):
+        T.assert_close_f32(got[k].cpu().numpy(), ora[k])
+    ref_h.close(), h.close()
+
+
+def test_set_batch_mid_stream_keeps_state():
+    """Changing the batch between frames carries G_{t-1} over."""
+    import torch
+    import mm355
+    W, H = 200, 120
+    fr = T.synth(W, H, 8)
+    dev = _dev(fr)
+    p = mm355.Params.make(phase_scale=25.0)
+    ref = _stream(mm355.Handle(W, H, p), dev, mm355.RGBA32F, [8])
+    h = mm355.Handle(W, H, p)
+    h.set_batch(2)
+    out = torch.empty_like(dev)
+    h.process_stream(dev[:3], out[:3], 3, mm355.RGBA32F)
+    h.set_batch(7)
+    h.process_stream(dev[3:], out[3:], 5, mm355.RGBA32F)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    h.close()
+
+
+def test_debug_view_after_batch_growth():
+    """a debug view at batch 1, then batch 8 and an 8-frame
+    debug stream: the view textures grow with the batch (no write past them)
+    and the frames equal a fresh handle's at batch 8."""
+    import torch
+    import mm355
+    W, H = 64, 48
+    fr = T.synth(W, H, 9)
+    dev = _dev(fr)
+    p = mm355.Params.make(phase_scale=10.0, show_magnitude=True)
+    h = mm355.Handle(W, H, p)
+    h.set_batch(1)
+    out = torch.empty_like(dev)
+    h.process(dev[0], out[0], mm355.RGBA32F)
+    h.set_batch(8)
+    h.process_stream(dev[1:], out[1:], 8, mm355.RGBA32F)
+    torch.cuda.synchronize()
+    ref = _stream(mm355.Handle(W, H, p), dev, mm355.RGBA32F, [9])
+    assert torch.equal(out, ref)
+    ora = T.oracle_run(W, H, fr, 5, 10.0, debug=(True, False))
+    for k in range(1, 9):
+        e = np.abs(out[k].cpu().numpy()[..., 0].astype(np.float64) - ora[k][..., 0])
+        assert e.max() < 1e-4
+    h.close()
+
+
+def test_steerable_set_batch_mid_stream():
+    """mm_set_batch mid-stream must not drop or corrupt the
+    steerable local-phase state: equal, bitwise, to the uninterrupted stream."""
+    import torch
+    import mm355
+    W, H = 96, 64
+    fr = T.synth(W, H, 7)
+    dev = _dev(fr)
+    p = mm355.Params.make(levels=5, phase_scale=10.0, mode=mm355.MODE_STEERABLE, orientations=8)
+    ref_h = mm355.Handle(W, H, p)
+    ref_h.set_batch(2)
+    ref = _stream(ref_h, dev, mm355.RGBA32F, [7])
+    h = mm355.Handle(W, H, p)
+    h.set_batch(2)
+    out = torch.empty_like(dev)
+    h.process_stream(dev[:3], out[:3], 3, mm355.RGBA32F)
+    h.set_batch(5)                      # grows the per-batch spectra, keeps the planes
+    h.process_stream(dev[3:], out[3:], 4, mm355.RGBA32F)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # and with a mm_set_state in between
+    st = torch.empty(h.state_bytes, dtype=torch.uint8, device="cuda")
+    g = mm355.Handle(W, H, p)
+    g.set_batch(3)
+    o2 = torch.empty_like(dev)
+    g.process_stream(dev[:4], o2[:4], 4, mm355.RGBA32F)
+    g.get_state(st)
+    g.set_batch(1)
+    g.set_state(st)
+    g.process_stream(dev[4:], o2[4:], 3, mm355.RGBA32F)
+    torch.cuda.synchronize()
+    assert torch.equal(o2, ref)
+    ref_h.close(), h.close(), g.close()
+
+
+def test_set_params_does_not_stall_other_streams():
+    """mm_set_params waits only for its own handle's work:
+    while handle B's long stream runs on its own stream, A's edge-mode change
+    returns before B's work is done; A's next frames use the new tables."""
+    import torch
+    import mm355
+    W, H = 1920, 1080
+    pb = mm355.Params.make(phase_scale=25.0)
+    b = mm355.Handle(W, H, pb)
+    b.set_batch(64)
+    frames = torch.empty((64, H, W, 4), dtype=torch.uint8, device="cuda")
+    b.synth(frames, 0, 64)
+    outb = torch.empty_like(frames)
+    torch.cuda.synchronize()
+    sb = torch.cuda.Stream()
+    Wa, Ha = 64, 48
+    fr = T.synth(Wa, Ha, 3)
+    a = mm355.Handle(Wa, Ha, mm355.Params.make(phase_scale=10.0))
+    dev = _dev(fr)
+    oa = torch.empty_like(dev)
+    a.process(dev[0], oa[0], mm355.RGBA32F)
+    torch.cuda.synchronize()
+    for _ in range(8):                                      # ~10 ms of work on sb
+        b.process_stream(frames, outb, 64, mm355.RGBA8, stream=sb.cuda_stream)
+    t0 = time.perf_counter()
+    a.set_params(mm355.Params.make(phase_scale=10.0, edge_mode=mm355.EDGE_CLAMP))
+    dt = time.perf_counter() - t0
+    busy = not sb.query()
+    torch.cuda.synchronize()
+    assert busy, f"B's stream finished before mm_set_params returned ({dt * 1e3:.2f} ms)"
+    a.process(dev[1], oa[1], mm355.RGBA32F)
+    a.process(dev[2], oa[2], mm355.RGBA32F)
+    torch.cuda.synchronize()
+    # frame 2 and its state (frame 1) both ran on the CLAMP tables (frame 1
+    # itself pairs the old REPEAT state with the new tables: the state is the
+    # previous frame's resampled rows)
+    ref = T.oracle_run(Wa, Ha, fr, 5, 10.0, edge=1)
+    T.assert_close_f32(oa[2].cpu().numpy(), ref[2])
+    a.close(), b.close()
+
+
+@pytest.mark.parametrize("W,H,L,S,edge", [(16, 12, 3, 10.0, 0), (12, 10, 4, 25.0, 1), (13, 9, 5, 10.0, 0),
+                                          (16, 16, 5, 25.0, 1), (9, 16, 2, 10.0, 0)])
+def test_smallest_canvas_n16(W, H, L, S, edge):
+    """N = 16, the smallest canvas of the build (9 <= max(W, H) <= 16), on
+    the oracle's canvas (no clamp: VERDICT r2 #7), frame and stream calls."""
+    fr = T.synth(W, H, 5)
+    ref = T.oracle_run(W, H, fr, L, S, edge)
+    for mode in ("frame", "stream"):
+        got = T.gpu_run(W, H, fr, L, S, edge, mode=mode, batch=2)
+        assert np.array_equal(got[0], fr[0])
+        for g, r in zip(got[1:], ref[1:]):
+            T.assert_close_f32(g, r)
+
+
+def test_refused_geometries():
+    """max(W, H) <= 8 (N <= 8) and N = 8192 are refused with
+    MM_ERR_UNSUPPORTED, not computed on another canvas."""
+    import mm355
+    for W, H in ((8, 6), (4, 4), (2, 8), (4097, 2160), (8192, 4320)):
+        with pytest.raises(mm355.MMError) as ei:
+            mm355.Handle(W, H)
+        assert ei.value.code == -2, (W, H)

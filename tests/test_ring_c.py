@@ -70,3 +70,30 @@ def test_c_ring_world1_equals_single_stream(tmp_path):
     assert ring.returncode == 0, ring.stdout + ring.stderr
     a, b = _checksums(one.stdout), _checksums(ring.stdout)
     assert len(a) == 48 and a == b
+
+
+def _bench(args):
+    import json
+    import sys
+    env = dict(os.environ, NCCL_DEBUG="WARN", PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+def test_bench_c_ring_world1_1080p_equals_single_rank():
+    """bench.py's N>1 ring path is the C ring: at world 1
+    (--ring-self) every step's state goes through libmm_ring's RCCL
+    send/receive to the same rank; at 1920x1080 the per-frame output
+    checksums of 3 steps x 8 frames equal the plain single-rank stream."""
+    common = ["--checksum", "--frames-per-step", "8", "--steps", "2", "--warmup", "1"]
+    one = _bench(common)
+    ring = _bench(common + ["--ring-self"])
+    assert one["frames"] == ring["frames"] == [0, 23]
+    assert one["checksums"] == ring["checksums"]
+    line = _bench(["--ring-self", "--frames-per-step", "16", "--steps", "2", "--warmup", "1",
+                   "--no-cpu-baseline", "--drop-in-frames", "0"])
+    assert "C host RCCL ring" in line["config"]["parallelism"], line["config"]
+    assert line["value"] > 0
