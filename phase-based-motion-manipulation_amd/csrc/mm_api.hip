@@ -1024,7 +1024,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.edge = p->edge_mode;
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
-    h->k2_pow = h->spec.S_pow >= 0 && !getenv("MM_K2_NOPOW");
+    h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
@@ -1097,7 +1097,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
-    h->k2_pow = h->spec.S_pow >= 0 && !getenv("MM_K2_NOPOW");
+    h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
     if (edge_changed) return upload_tables(h);
     return MM_OK;
 }

@@ -552,8 +552,11 @@ constexpr int MM_K2_PYR_TAB = 2;
 // (wrap subtracts a multiple of 2 pi, which an integer S maps to a multiple
 // of 2 pi: PyramidPhaseDifference.compute:47-54, 92-98).  z^|S| by square and
 // multiply over the bits of |S| (a uniform scalar loop), conj for S < 0.
-// Same value up to fp32 rounding (measured against the oracle's atan2f path:
-// tests/test_k2_pow.py); non-integer S keeps the atan2 form.
+// Same value up to fp32 rounding (tests/test_k2_pow.py, against the atan2
+// form and the oracle's atan2f path); non-integer S keeps the atan2 form.
+// Opt-in (MM_K2_POW=1): same-call 4 % slower than the atan2 form in spite of
+// fewer issue slots (the scalar bit loop and its phi moves break the bins'
+// interleaving; profiles/r03_ab3.txt).
 constexpr int MM_K2_PYR_POW = 3;
 template <int MODE> constexpr bool k2_tabled() { return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_POW; }
 
@@ -887,14 +890,13 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     // frame-invariant bases plus immediates (k2_tix): entry fy0 + m C at slot
     // k2_tix(fy0) + m, entry M - fy0 (M a multiple of C) at slot
     // k2_tix(C - w) - 1 - fy0 / C + M / C for w = fy0 mod C > 0.
-    const float2 *tlo0, *thi0;
-    {
-        constexpr int C = fft_c_v(LOG2N);
-        const int fy0 = fft_bin<LOG2N>(t0, 0);
-        const int w = fy0 % C;
-        tlo0 = tab0 + k2_tix<LOG2N>(fy0);
-        thi0 = tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
-    }
+    // (hoisted out of the frame loop where registers allow: N >= 2048, TK == 2;
+    // smaller N recompute them per frame from the opaque lane index)
+    constexpr bool HOIST = q_tile<LOG2N>() == 2;
+    const int hfy0 = fft_bin<LOG2N>(t0, 0);
+    const int hw = hfy0 % fft_c_v(LOG2N);
+    const float2 *tlo0 = tab0 + k2_tix<LOG2N>(hfy0);
+    const float2 *thi0 = tab0 + (hw ? k2_tix<LOG2N>(fft_c_v(LOG2N) - hw) - 1 : 0) - hfy0 / fft_c_v(LOG2N);
 
     // G column of a frame.  Rows outside the image get an out-of-range buffer
     // offset: the range check returns 0 for them without a memory access (the
@@ -987,7 +989,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         if (blk0) __builtin_amdgcn_s_setprio(3);
         else if ((fr ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
+#ifdef MM_K2_NOGAHEAD
         load_g(fr < nframes ? fr : nframes - 1, t);
+#else
+        if (fr < 0) load_g(-1, t);   // Gprev; later frames' loads were issued mid-iteration
+#endif
         K2_STAMP(0);
         __builtin_amdgcn_sched_barrier(0);   // keep the stores behind the loads
         {
@@ -998,12 +1004,24 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             const int qfr = __builtin_amdgcn_readfirstlane(fr > 0 ? fr - 1 : 0);   // uniform
             const auto qrs = __builtin_amdgcn_make_buffer_rsrc(
                 Q + (size_t)qfr * q_stride, 0, staged ? (int)(q_stride * sizeof(c2)) : 0, 0x00020000);
+            unsigned so[NST];
+#pragma unroll
+            for (int i = 0; i < NST; ++i) {
+                if constexpr (HOIST) {
+                    so[i] = so_st[i];
+                } else {   // per frame from the opaque t (registers)
+                    const int e = grp * T + t + i * GPW * T;
+                    const int kt = e / BLK, r = e - kt * BLK;
+                    const bool ok = e < nq && (GPW <= N / 2 || fb + (2 * r) / TK < N / 2);
+                    so[i] = ok ? (unsigned)((kt * g.Qs + fb) * TK + 2 * r) * 8u : 0x80000000u;
+                }
+            }
 #pragma unroll
             for (int i = 0; i < NST; ++i) {
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                 const u32x4 d = {__float_as_uint(sv[i].x), __float_as_uint(sv[i].y),
                                  __float_as_uint(sv[i].z), __float_as_uint(sv[i].w)};
-                __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so_st[i], 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so[i], 0, 0);
             }
             // column N/2 of frame fr-1 (block 0 only).  Read after the barrier:
             // stgN is rewritten only after the packed section's first barrier below.
@@ -1048,7 +1066,10 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                 // integer phase scale: the power form, two bins at a time (the
                 // table addressing of the branch above)
                 constexpr int C = fft_c_v(LOG2N);
-                const float2 *tlo = tlo0, *thi = thi0;   // (frame-invariant: hoisted)
+                const int fy0 = fft_bin<LOG2N>(HOIST ? t0 : t, 0);   // frame-invariant (hoisted: t0)
+                const int w = fy0 % C;
+                const float2 *tlo = HOIST ? tlo0 : tab0 + k2_tix<LOG2N>(fy0);
+                const float2 *thi = HOIST ? thi0 : tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
 #ifndef MM_K2_POWG
 #define MM_K2_POWG 4   // bins per power loop (its scalar control and phi moves amortise over them; 8 spills)
 #endif
@@ -1072,7 +1093,10 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                 // k2_tix(fy0) + m, entry M - fy0 (M a multiple of C) at slot
                 // k2_tix(C - w) - 1 - fy0 / C + M / C for w = fy0 mod C > 0.
                 constexpr int C = fft_c_v(LOG2N);
-                const float2 *tlo = tlo0, *thi = thi0;   // (frame-invariant: hoisted)
+                const int fy0 = fft_bin<LOG2N>(HOIST ? t0 : t, 0);   // frame-invariant (hoisted: t0)
+                const int w = fy0 % C;
+                const float2 *tlo = HOIST ? tlo0 : tab0 + k2_tix<LOG2N>(fy0);
+                const float2 *thi = HOIST ? thi0 : tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
@@ -1201,6 +1225,13 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             __syncthreads();   // the inverse FFT rewrites the buffer
         }
         if constexpr (!blk0) regular_op();
+#ifndef MM_K2_NOGAHEAD
+        // next frame's G loads now: they land during this frame's inverse
+        // transform, staging and Q stores instead of stalling the next frame
+        // at its top (same-call K2 8.94 -> 8.33 us/frame, profiles/r03_abv.txt;
+        // the op's registers are free again here: no spill at 123 VGPRs)
+        load_g(fr + 1 < nframes ? fr + 1 : nframes - 1, t);
+#endif
         staged = !pass_frame;
         if (!pass_frame) {
         K2_STAMP(4);

@@ -1,9 +1,16 @@
-# parity suite on the default build, then interleaved A/B of lib/variants/*.so
+# Same-call A/B of compiled variants lib/variants/*.so (bench batch pattern and
+# optionally per-frame), R rounds.  usage: bash scripts/gpu_abv.sh ROUNDS [pf]
 set -o pipefail
-R=$GRAFT_REPO_ROOT; cd $R; export TMPDIR=/tmp; TAG=${1:-abv}
-timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/${TAG}_tests.log 2>&1 || { echo TEST FAIL; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
-tail -1 gpurun_out/${TAG}_tests.log
-for round in 1 2; do
-for v in phase-based-motion-manipulation_amd/lib/variants/*.so; do
-  timeout -k 10 200 env MM355_LIB=$R/$v python bench.py --no-cpu-baseline ${BENCH_ARGS:-} 2>/dev/null | python3 -c "import json,sys; d=json.load(sys.stdin); print('$(basename $v)', d['value'], {k:v['us_per_frame'] for k,v in d['kernels'].items()})" || { echo "$v FAIL"; exit 1; }
-done; done
+R=$GRAFT_REPO_ROOT; cd $R; N=${1:-2}; PF=$2
+for i in $(seq $N); do
+  for V in phase-based-motion-manipulation_amd/lib/variants/*.so; do
+    n=$(basename $V .so)
+    MM355_LIB=$R/$V timeout -k 10 240 python bench.py --no-cpu-baseline --drop-in-frames 0 --steps 5 > gpurun_out/abv_$n.json 2> gpurun_out/abv_$n.err || { echo BENCH FAIL $n; tail gpurun_out/abv_$n.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], {k: v['us_per_frame'] for k, v in d['kernels'].items()})" gpurun_out/abv_$n.json $n
+    if [ -n "$PF" ]; then
+      MM355_LIB=$R/$V timeout -k 10 240 python bench.py --no-cpu-baseline --steps 1 --warmup 1 --frames-per-step 100 > gpurun_out/abvpf_$n.json 2> gpurun_out/abvpf_$n.err || { echo PF FAIL $n; tail gpurun_out/abvpf_$n.err; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1]))['drop_in_per_frame']; print(sys.argv[2], 'drop-in', d['frames_per_s'], d['latency_ms'])" gpurun_out/abvpf_$n.json $n
+    fi
+  done
+done
+echo ALL OK
