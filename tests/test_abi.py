@@ -100,3 +100,21 @@ def test_processor_params_mirror_inspector_fields():
     s = P(64, 48, orientations=4, temporal_filter=mm355.FILTER_IIR, iir_low=0.1, iir_high=0.5)._params()
     assert (s.mode, s.orientations, s.temporal_filter) == (mm355.MODE_STEERABLE, 4, mm355.FILTER_IIR)
     assert abs(s.iir_low - 0.1) < 1e-7 and abs(s.iir_high - 0.5) < 1e-7
+
+
+def test_unity_shim_calls_only_declared_entry_points():
+    """The Unity rendering-plugin shim (source only: no Unity/Vulkan SDK here)
+    calls only entry points include/mm.h declares and the library exports."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(mm355.LIB_PATH), "..", "unity", "mm_unity_plugin.c")).read()
+    body = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    called = set(re.findall(r"\b(mm_[a-z_0-9]+)\s*\(", body))
+    own = {"mm_unity_create", "mm_unity_event_func", "mm_unity_destroy"}
+    declared = set(mm355.abi_symbols())
+    assert own <= called
+    assert called - own <= declared, called - own - declared
+    for s in called - own:
+        assert hasattr(mm355.lib(), s)
+    for entry in ("UnityPluginLoad", "UnityPluginUnload", "IssuePluginEventAndData"):
+        assert entry in src
