@@ -247,6 +247,32 @@ __device__ __forceinline__ float2 chroma_iq(typename Pix<FMT>::raw_t u)
     }
 }
 
+// Packed-FP32 pixel math of the compose stage (K4 and K34 share it, so the
+// fused and unfused outputs stay bitwise equal): (I, Q) is one c2, and every
+// weighted sum is written in the same left-to-right order as its scalar form,
+// so each lane computes the scalar form's fma chain exactly (v_pk_fma_f32 /
+// v_pk_mul_f32 with a broadcast scalar operand: half the VALU instructions).
+template <int FMT>
+__device__ __forceinline__ c2 chroma_iq2(typename Pix<FMT>::raw_t u)
+{
+    if constexpr (FMT == 0) {
+        constexpr float k = 1.0f / 255.0f;
+        const float r = (float)(u & 255u), gg = (float)((u >> 8) & 255u), b = (float)((u >> 16) & 255u);
+        return mk(0.596f * k, 0.211f * k) * r + mk(-0.274f * k, -0.523f * k) * gg + mk(-0.322f * k, 0.312f * k) * b;
+    } else {
+        return mk(0.596f, 0.211f) * u.x + mk(-0.274f, -0.523f) * u.y + mk(-0.322f, 0.312f) * u.z;
+    }
+}
+
+// YIQToRGB.shader:51-76 + saturate for one pixel: R and G as one pair, B alone
+__device__ __forceinline__ void yiq_rgb(float yb, c2 cc, float &rr, float &gg, float &bb)
+{
+    const c2 rg = mk(yb, yb) + mk(0.956f, -0.272f) * cc.x + mk(0.621f, -0.647f) * cc.y;
+    rr = sat(rg.x);
+    gg = sat(rg.y);
+    bb = sat(1.0f * yb + -1.106f * cc.x + 1.703f * cc.y);
+}
+
 // =========================================================================
 // K1: luma rows -> half spectra of row pairs
 // =========================================================================
@@ -277,7 +303,8 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     // vertical part of the separable resample: V_a, V_b over all source columns.
     // Taps of image row r lie on source rows r-1..r+1 (w3 tables), so the pair
     // (ra, ra+1) reads the 4 source rows ra-1..ra+2.
-    float *V = reinterpret_cast<float *>(lds);
+    float *V = reinterpret_cast<float *>(lds);   // GEN: [2][W] (rows a, b)
+    c2 *V2 = lds;                                 // 3-tap path: [W] (row a, row b) pairs
     using raw_t = typename Pix<FMT>::raw_t;
     constexpr int BPP = Pix<FMT>::bpp;
     // RGBA8: all 32 pixel loads of the thread in one batch; RGBA32F (4x the
@@ -314,6 +341,10 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         float4 wa = rowW3[ra], wb = ra + 1 < g.H ? rowW3[ra + 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         wa.x *= kLumaUnit<FMT>, wa.y *= kLumaUnit<FMT>, wa.z *= kLumaUnit<FMT>;
         wb.x *= kLumaUnit<FMT>, wb.y *= kLumaUnit<FMT>, wb.z *= kLumaUnit<FMT>;
+        // rows a and b as one packed pair: (a, b) = (wa.x, wb.x) (l0, l1) +
+        // (wa.y, wb.y) (l1, l2) + (wa.z, wb.z) (l2, l3), per lane the scalar
+        // forms' fma chains (half the VALU instructions, one 8-B LDS store)
+        const c2 w0 = mk(wa.x, wb.x), w1 = mk(wa.y, wb.y), w2 = mk(wa.z, wb.z);
         const uint8_t *rowp[4];   // workgroup-uniform source row pointers
 #pragma unroll
         for (int d = 0; d < 4; ++d) rowp[d] = img + (unsigned)(wrap_near(ra - 1 + d, g.H, g.edge) * g.W * BPP);
@@ -334,10 +365,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
                 float l[4];
 #pragma unroll
                 for (int d = 0; d < 4; ++d) l[d] = luma_units<FMT>(px[u][d]);
-                if (i < g.W) {
-                    V[i] = wa.x * l[0] + wa.y * l[1] + wa.z * l[2];
-                    V[g.W + i] = wb.x * l[1] + wb.y * l[2] + wb.z * l[3];
-                }
+                if (i < g.W) V2[i] = w0 * mk(l[0], l[1]) + w1 * mk(l[1], l[2]) + w2 * mk(l[2], l[3]);
             }
         }
     }
@@ -362,8 +390,9 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
             const float4 w = colW3[ic];   // weights of source columns i-1, i, i+1; .w: wrapped
             const unsigned nb = __float_as_uint(w.w);          // (i-1) | (i+1) << 16
             const int cl = nb & 0xffffu, cr = nb >> 16;
-            ya = w.x * V[cl] + w.y * V[ic] + w.z * V[cr];
-            yb = w.x * V[g.W + cl] + w.y * V[g.W + ic] + w.z * V[g.W + cr];
+            const c2 y2 = w.x * V2[cl] + w.y * V2[ic] + w.z * V2[cr];   // (ya, yb)
+            ya = y2.x;
+            yb = y2.y;
         }
         const bool in = valid && i >= 0 && i < g.W;
         v[j] = in ? mk(ya, yb) : mk(0.0f, 0.0f);
@@ -1460,7 +1489,7 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
                const float4 *__restrict__ rowW3)
 {
     constexpr int TR = kTileRows, TC = kTileCols, WC = TC + 2;
-    __shared__ float2 iq[(TR + 2) * WC];     // I/Q of the staged source pixels
+    __shared__ c2 iq[(TR + 2) * WC];         // I/Q of the staged source pixels
     const int tid = threadIdx.x;
     int b = blockIdx.x;
     const int ct = b % col_tiles;
@@ -1507,17 +1536,16 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
     const int hrow = wrap_near(min(i0 - 1 + (hs >> 1), g.H), g.H, g.edge);
     const int hcol = wrap_near(min(c0 - 1 + TC + (hs & 1), g.W), g.W, g.edge);
     const raw_t ph = ld_off<raw_t>(img, (unsigned)(hrow * g.W + hcol) * Pix<FMT>::bpp);
-    if (tid < NH) iq[(hs >> 1) * WC + TC + (hs & 1)] = chroma_iq<FMT>(ph);
+    if (tid < NH) iq[(hs >> 1) * WC + TC + (hs & 1)] = chroma_iq2<FMT>(ph);
 #pragma unroll
-    for (int sr = 0; sr < TR + 2; ++sr) iq[sr * WC + tid] = chroma_iq<FMT>(pa[sr]);
+    for (int sr = 0; sr < TR + 2; ++sr) iq[sr * WC + tid] = chroma_iq2<FMT>(pa[sr]);
     __syncthreads();
     if (!vx) return;
-    float hi[TR + 2], hq[TR + 2];
+    c2 hc[TR + 2];   // horizontally combined (I, Q) of each staged row
 #pragma unroll
     for (int sr = 0; sr < TR + 2; ++sr) {
-        const float2 a = iq[sr * WC + tid], m = iq[sr * WC + tid + 1], c = iq[sr * WC + tid + 2];
-        hi[sr] = wc.x * a.x + wc.y * m.x + wc.z * c.x;
-        hq[sr] = wc.x * a.y + wc.y * m.y + wc.z * c.y;
+        const c2 a = iq[sr * WC + tid], m = iq[sr * WC + tid + 1], c = iq[sr * WC + tid + 2];
+        hc[sr] = wc.x * a + wc.y * m + wc.z * c;
     }
     uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
 #pragma unroll
@@ -1525,14 +1553,11 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
         const int i = i0 + r;
         if (i < g.H) {
             const float4 wr = rowW3[i];                        // source rows i-1, i, i+1
-            const float ci = wr.x * hi[r] + wr.y * hi[r + 1] + wr.z * hi[r + 2];
-            const float cq = wr.x * hq[r] + wr.y * hq[r + 1] + wr.z * hq[r + 2];
+            const c2 cc = wr.x * hc[r] + wr.y * hc[r + 1] + wr.z * hc[r + 2];   // (ci, cq)
             const float yb = bw.w0 * yv[r + 2] + bw.w1 * (yv[r + 1] + yv[r + 3]) +
                              bw.w2 * (yv[r] + yv[r + 4]);
-            // YIQToRGB.shader:51-76 + saturate
-            const float rr = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
-            const float gg = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
-            const float bb = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
+            float rr, gg, bb;
+            yiq_rgb(yb, cc, rr, gg, bb);
             Pix<FMT>::store(outp + (unsigned)(i * g.W * Pix<FMT>::bpp), (unsigned)X, rr, gg, bb);
         }
     }
@@ -1583,7 +1608,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
     const unsigned cr = (unsigned)wrap_near(X + 4, g.W, g.edge);
     // horizontally combined I/Q of one source row for the quad (k_compose's
     // staged 3-tap combine over columns X-1 .. X+4)
-    auto chroma_row = [&](int i, float (&hi)[4], float (&hq)[4]) {
+    auto chroma_row = [&](int i, c2 (&hc)[4]) {
         const int row = wrap_near(min(i, g.H), g.H, g.edge);
         const unsigned base = (unsigned)(row * g.W);
         raw_t p[6];
@@ -1596,21 +1621,21 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
             for (int k = 0; k < 4; ++k) p[1 + k] = ld_off<raw_t>(img, (base + (unsigned)X + k) * bpp);
         }
         p[5] = ld_off<raw_t>(img, (base + cr) * bpp);
-        float2 a[6];
+        c2 a[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) a[k] = chroma_iq<FMT>(p[k]);
+        for (int k = 0; k < 6; ++k) a[k] = chroma_iq2<FMT>(p[k]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float4 wc = colW3[X + k];
-            hi[k] = wc.x * a[k].x + wc.y * a[k + 1].x + wc.z * a[k + 2].x;
-            hq[k] = wc.x * a[k].y + wc.y * a[k + 1].y + wc.z * a[k + 2].y;
+            hc[k] = wc.x * a[k] + wc.y * a[k + 1] + wc.z * a[k + 2];
         }
     };
 
     float yw[8][4];            // list rows i0+4s-4 .. i0+4s+3 of the quad (blurred horizontally)
-    float hi[6][4], hq[6][4];  // combined I/Q of source rows i0+4s-5 .. i0+4s
-    chroma_row(i0 - 1, hi[4], hq[4]);
-    chroma_row(i0, hi[5], hq[5]);
+                               // (as column pairs for a packed vertical blur: +3 spills, not kept)
+    c2 hc[6][4];               // combined (I, Q) of source rows i0+4s-5 .. i0+4s
+    chroma_row(i0 - 1, hc[4]);
+    chroma_row(i0, hc[5]);
     for (int s = 0; s < steps; ++s) {
         // ---- K3 on list-row pair i0/2 + 2s + grp (zero beyond Hn) ----
         const int ka = i0 + 4 * s + 2 * grp;
@@ -1658,7 +1683,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         if (s > 0) {
             // ---- K4 on output rows i0+4s-4 .. i0+4s-1 ----
 #pragma unroll
-            for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hi[2 + r], hq[2 + r]);
+            for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + 4 * s - 4 + r;
@@ -1667,13 +1692,10 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
                     float rr[4], gg[4], bb[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        const float ci = wr.x * hi[r][k] + wr.y * hi[r + 1][k] + wr.z * hi[r + 2][k];
-                        const float cq = wr.x * hq[r][k] + wr.y * hq[r + 1][k] + wr.z * hq[r + 2][k];
+                        const c2 cc = wr.x * hc[r][k] + wr.y * hc[r + 1][k] + wr.z * hc[r + 2][k];
                         const float yb = bw.w0 * yw[r + 2][k] + bw.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
                                          bw.w2 * (yw[r][k] + yw[r + 4][k]);
-                        rr[k] = sat(1.0f * yb + 0.956f * ci + 0.621f * cq);
-                        gg[k] = sat(1.0f * yb + -0.272f * ci + -0.647f * cq);
-                        bb[k] = sat(1.0f * yb + -1.106f * ci + 1.703f * cq);
+                        yiq_rgb(yb, cc, rr[k], gg[k], bb[k]);
                     }
                     const unsigned o = (unsigned)(i * g.W + X);
                     if constexpr (FMT == 0) {
@@ -1698,8 +1720,8 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
             for (int k = 0; k < 4; ++k) yw[r][k] = yw[4 + r][k];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            hi[0][k] = hi[4][k]; hq[0][k] = hq[4][k];
-            hi[1][k] = hi[5][k]; hq[1][k] = hq[5][k];
+            hc[0][k] = hc[4][k];
+            hc[1][k] = hc[5][k];
         }
     }
 }
