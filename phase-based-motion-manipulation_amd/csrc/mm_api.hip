@@ -1348,6 +1348,15 @@ int mm_synth_frames(void *dev_out, int width, int height, int t0, int count, uin
     return MM_OK;
 }
 
+#ifdef MM_K34_STAMPS
+// diagnostic builds only (not in include/mm.h): k_rows_inv_compose phase cycle totals per wave
+int mm_debug_k34_stamps(unsigned long long *host, int n)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(mm_k34_stamps), sizeof(unsigned long long) * n) == hipSuccess
+               ? MM_OK : MM_ERR_HIP;
+}
+#endif
+
 #ifdef MM_K2_STAMPS
 // diagnostic builds only (not in include/mm.h): k_cols phase cycle totals per wave
 int mm_debug_k2_stamps(unsigned long long *host, int n)

@@ -1577,6 +1577,19 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
 // k_compose does (same expressions).  Yh never goes through HBM: the frame
 // saves its write and re-read (2 x 4 Hn W bytes); a strip re-transforms 4
 // halo rows (4 / R more Q reads and FFT work).
+#ifdef MM_K34_STAMPS
+// Diagnostic build only: per-wave cycle totals of the strip-step phases
+// (s_memtime deltas), written by lane 0 with a vector store after the walk.
+__device__ unsigned long long mm_k34_stamps[65536 * 8];
+#define K34_STAMP(i)                                                     \
+    do {                                                                 \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();      \
+        st_acc[i] += n_ - st_prev;                                       \
+        st_prev = n_;                                                    \
+    } while (0)
+#else
+#define K34_STAMP(i) do { } while (0)
+#endif
 template <int LOG2N, int FMT>
 __global__ __launch_bounds__(2 * fft_T<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
@@ -1636,6 +1649,11 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
     c2 hc[6][4];               // combined (I, Q) of source rows i0+4s-5 .. i0+4s
     chroma_row(i0 - 1, hc[4]);
     chroma_row(i0, hc[5]);
+#ifdef MM_K34_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+    st_acc[7] = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int s = 0; s < steps; ++s) {
         // ---- K3 on list-row pair i0/2 + 2s + grp (zero beyond Hn) ----
         const int ka = i0 + 4 * s + 2 * grp;
@@ -1660,7 +1678,9 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
             if (mirror) { qq.y = -qq.y; qq.w = -qq.w; }
             v[j] = valid ? mk(qq.x - qq.w, qq.y + qq.z) : mk(0.0f, 0.0f);
         }
+        K34_STAMP(0);
         fft_regs<LOG2N, +1>(v, t, lds, tw);
+        K34_STAMP(1);
         float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows ka, ka+1
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1668,6 +1688,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
             raw[N + t + j * T] = fabsf(v[j].y);
         }
         __syncthreads();
+        K34_STAMP(2);
         // ---- horizontal blur of the 4 new list rows (k_rows_inv's float4 form) ----
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1680,10 +1701,12 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
             yw[4 + r][3] = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
         }
         __syncthreads();   // LDS free for the next step's FFT
+        K34_STAMP(3);
         if (s > 0) {
             // ---- K4 on output rows i0+4s-4 .. i0+4s-1 ----
 #pragma unroll
             for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
+            K34_STAMP(4);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + 4 * s - 4 + r;
@@ -1712,6 +1735,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
                 }
             }
         }
+        K34_STAMP(5);
         // ---- slide: keep list rows i0+4s .. +3 and source rows i0+4s-1, i0+4s
         // (after step 0: the primed rows i0-1, i0) ----
 #pragma unroll
@@ -1724,6 +1748,13 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
             hc[1][k] = hc[5][k];
         }
     }
+#ifdef MM_K34_STAMPS
+    st_acc[6] = (unsigned long long)steps;
+    st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
+    const int w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (threadIdx.x % 64 == 0 && w < 65536)
+        for (int i = 0; i < 8; ++i) mm_k34_stamps[w * 8 + i] = st_acc[i];
+#endif
 }
 
 // K4 for odd W and/or H: the quad's edge then sits half a texel off the
