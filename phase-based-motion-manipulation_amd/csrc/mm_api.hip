@@ -44,6 +44,8 @@ struct mm_handle {
     Tap4 *d_col, *d_row;
     float4 *d_col3, *d_row3;    // the same taps merged onto offsets -1, 0, +1
     c2 *d_tw;
+    float2 *d_ktab;             // K2's per-bin tables of every column (k_k2_table)
+    int ktab_mode;              // table kind d_ktab holds (-1: stale, refilled before the next K2)
     c2 *d_tw_half;              // W_{N/2} table (debug views, lazily)
     float *d_dbg;               // debug view textures [dbg_frames][mag, phase][N][N] (lazily)
     // MM_MODE_STEERABLE (lazily, for the current levels/orientations):
@@ -307,6 +309,13 @@ static int validate_params(const mm_params *p)
 // ------------------------------------------------------------------------
 // launches
 // ------------------------------------------------------------------------
+// slots of one column of K2's per-bin table (k2_tab_slots)
+static constexpr int ktab_slots(int log2n)
+{
+    const int C = fft_c_v(log2n), te = (1 << log2n) / 2 + 1;
+    return (te + C - 1) / C * C;
+}
+
 static int ilog2(int n)
 {
     int l = 0;
@@ -373,6 +382,20 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
     const int gpw = k2_groups<LOG2N>();
     const int cols = (1 << LOG2N) / 2;   // f = 0 and f = N/2 share group 0 (k_cols)
     const int blocks = (cols + gpw - 1) / gpw;
+    // the per-bin tables, stream-ordered before this launch after a parameter change
+    static_assert(ktab_slots(LOG2N) == k2_tab_slots<LOG2N>(), "d_ktab column stride");
+    const int tab_mode = h->spec.mode == MM_MODE_STANDARD ? MM_MODE_STANDARD : h->k2_tab ? MM_K2_PYR_TAB : -1;
+    if (tab_mode >= 0 && h->ktab_mode != tab_mode) {
+        const int n = (cols + 1) * k2_tab_slots<LOG2N>();
+        if (tab_mode == MM_MODE_STANDARD)
+            hipLaunchKernelGGL((k_k2_table<LOG2N, MM_MODE_STANDARD>), dim3((n + 255) / 256), dim3(256), 0, s,
+                               h->d_ktab, h->spec);
+        else
+            hipLaunchKernelGGL((k_k2_table<LOG2N, MM_K2_PYR_TAB>), dim3((n + 255) / 256), dim3(256), 0, s,
+                               h->d_ktab, h->spec);
+        HIPCHK(hipGetLastError());
+        h->ktab_mode = tab_mode;
+    }
     ProfScope ps(h, s, MM_K_COLS, nframes);
     // per group: FFT exchange buffer + two per-bin tables (k_cols)
     const size_t lds = k2_lds_bytes<LOG2N>();
@@ -382,11 +405,11 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
 #define MM_K2_LAUNCH(MODE)                                                                           \
     do {                                                                                             \
         hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, G, \
-                           h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, \
+                           h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, h->d_ktab, \
                            nframes - k);                                                             \
         if (k)                                                                                       \
             hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G, \
-                               h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw); \
+                               h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab); \
     } while (0)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
     else if (h->k2_tab && h->k2_pow) MM_K2_LAUNCH(MM_K2_PYR_POW);
@@ -863,6 +886,7 @@ static void free_handle(mm_handle *h)
     (void)hipFree(h->d_col3);
     (void)hipFree(h->d_row3);
     (void)hipFree(h->d_tw);
+    (void)hipFree(h->d_ktab);
     (void)hipFree(h->d_tw_half);
     (void)hipFree(h->d_dbg);
     (void)hipFree(h->d_Fb);
@@ -1025,6 +1049,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
+    h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
@@ -1044,6 +1069,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
               dev_alloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
               dev_alloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
               dev_alloc(&h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
+              dev_alloc(&h->d_ktab, sizeof(float2) * (size_t)(N / 2 + 1) * ktab_slots(h->log2n)) == hipSuccess &&
               alloc_batch(h, h->chunk) == MM_OK;
     if (!ok) {
         free_handle(h);
@@ -1098,6 +1124,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     build_spec(*p, h->N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
+    h->ktab_mode = -1;
     if (edge_changed) return upload_tables(h);
     return MM_OK;
 }
@@ -1362,6 +1389,11 @@ int mm_debug_k34_stamps(unsigned long long *host, int n)
 int mm_debug_k2_stamps(unsigned long long *host, int n)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(mm_k2_stamps), sizeof(unsigned long long) * n) == hipSuccess
+               ? MM_OK : MM_ERR_HIP;
+}
+int mm_debug_k2_entry(unsigned long long *host, int n)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(mm_k2_entry), sizeof(unsigned long long) * n) == hipSuccess
                ? MM_OK : MM_ERR_HIP;
 }
 #endif

@@ -307,6 +307,17 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     c2 *V2 = lds;                                 // 3-tap path: [W] (row a, row b) pairs
     using raw_t = typename Pix<FMT>::raw_t;
     constexpr int BPP = Pix<FMT>::bpp;
+    // one-pair workgroups (LAT: short launches, latency-bound) issue the
+    // column taps and twiddles with the pixel loads instead of one dependent
+    // round trip each after them (batch launches: K1 +5 %, registers held
+    // across the loads)
+    c2 wb[16];
+    float4 cw[8];
+    if constexpr (LAT && !GEN) {
+        preload_twiddles_wl<LOG2N>(wb, t, tw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cw[j] = colW3[min(max(t + j * T - g.x0, 0), g.W - 1)];
+    }
     // RGBA8: all 32 pixel loads of the thread in one batch; RGBA32F (4x the
     // registers): two batches of 16
     constexpr int UB = FMT == 0 ? 8 : 4;
@@ -387,7 +398,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
                 yb += tc.w[m] * V[g.W + c];
             }
         } else {
-            const float4 w = colW3[ic];   // weights of source columns i-1, i, i+1; .w: wrapped
+            const float4 w = LAT ? cw[j] : colW3[ic];   // weights of source columns i-1, i, i+1; .w: wrapped
             const unsigned nb = __float_as_uint(w.w);          // (i-1) | (i+1) << 16
             const int cl = nb & 0xffffu, cr = nb >> 16;
             const c2 y2 = w.x * V2[cl] + w.y * V2[ic] + w.z * V2[cr];   // (ya, yb)
@@ -397,8 +408,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
         const bool in = valid && i >= 0 && i < g.W;
         v[j] = in ? mk(ya, yb) : mk(0.0f, 0.0f);
     }
-    c2 wb[16];   // (issued at kernel start instead: K1 +5 %, registers held across the loads)
-    preload_twiddles_wl<LOG2N>(wb, t, tw);
+    if constexpr (!LAT || GEN) preload_twiddles_wl<LOG2N>(wb, t, tw);
     __syncthreads();
     fft_dif<LOG2N, -1>(v, t, lds, wb);
     __syncthreads();   // every wave done with its LDS region
@@ -834,6 +844,7 @@ template <int LOG2N> constexpr size_t k2_lds_bytes()
 // Diagnostic build only: per-wave cycle totals of the frame-loop phases
 // (s_memtime deltas), written by lane 0 with a vector store after the loop.
 __device__ unsigned long long mm_k2_stamps[4096 * 8 * 8];
+__device__ unsigned long long mm_k2_entry[4096 * 8];   // s_memrealtime at entry, per wave
 #define K2_STAMP(i)                                                      \
     do {                                                                 \
         const unsigned long long n_ = __builtin_amdgcn_s_memtime();      \
@@ -856,10 +867,14 @@ __device__ unsigned long long mm_k2_stamps[4096 * 8 * 8];
 template <int LOG2N, int MODE, bool BLK0>
 __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q,
                                             size_t q_stride, int nframes, const Geo &g,
-                                            const Spec &sp, const c2 *__restrict__ tw, int blk)
+                                            const Spec &sp, const c2 *__restrict__ tw,
+                                            const float2 *__restrict__ ktab, int blk)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     constexpr int TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
+#ifdef MM_K2_STAMPS
+    const unsigned long long st_entry = __builtin_amdgcn_s_memrealtime();
+#endif
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     // group index: wave-uniform (scalar) when a group spans whole waves
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
@@ -878,16 +893,19 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     constexpr bool blk0 = BLK0;               // block 0 runs the extra exchanges
     const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
 
+    // twiddle bases of both FFTs, loaded once (issued under the table copy): no loads inside a frame but G's
+    c2 wtw[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    preload_twiddles_wl<LOG2N>(wtw, t0, tw);
     if constexpr (MODE != MM_MODE_PYRAMID) {
-        for (int e = t0; e < TE; e += T) {
-            // pyramid table: masks pre-scaled by inv_nn (a power of two: exact)
-            const float ks = k2_tabled<MODE>() ? sp.inv_nn : 1.0f;
-            const float2 b0 = bin_static<LOG2N, MODE>(f, e, sp);
-            tab0[k2_tix<LOG2N>(e)] = make_float2(b0.x * ks, b0.y * ks);
-            if (packed) {
-                const float2 bn = bin_static<LOG2N, MODE>(N / 2, e, sp);
-                tabN[k2_tix<LOG2N>(e)] = make_float2(bn.x * ks, bn.y * ks);
-            }
+        // the column's table, evaluated once per parameter set by k_k2_table
+        // (slot order): a copy instead of N/2+1 bin_static per group and launch
+        const float2 *src0 = ktab + (size_t)f * TS;
+        for (int e = t0; e < TS; e += T) tab0[e] = src0[e];
+        if (packed) {
+            const float2 *srcN = ktab + (size_t)(N / 2) * TS;
+            for (int e = t0; e < TS; e += T) tabN[e] = srcN[e];
         }
         __syncthreads();
     }
@@ -960,11 +978,6 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                 gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, o0 + (unsigned)(j * T * 8), 0, 0));
         }
     };
-    // twiddle bases of both FFTs, loaded once: no loads inside a frame but G's
-    c2 wtw[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles_wl<LOG2N>(wtw, t0, tw);
     constexpr int TK = q_tile<LOG2N>(), BLK = GPW * TK / 2;   // float4 per tile row
     constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
     const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
@@ -1327,6 +1340,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         const int w = (blk0 && nframes == 1 && gridDim.x < 512 ? 4096 : 0) +
                       blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
         for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
+        mm_k2_entry[w] = st_entry;
     }
 #endif
 }
@@ -1338,15 +1352,16 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
-            int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, int nframes_blk0)
+            int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, const float2 *__restrict__ ktab,
+            int nframes_blk0)
 {
     // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
     // are merged in one L2 (split over XCDs they left as partial-line writes)
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     if (blk == 0)   // the packed block stops nframes_blk0 frames in (k_cols_tail)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, blk);
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, blk);
     else
-        k_cols_body<LOG2N, MODE, false>(G, g_stride, Gprev, Q, q_stride, nframes, g, sp, tw, blk);
+        k_cols_body<LOG2N, MODE, false>(G, g_stride, Gprev, Q, q_stride, nframes, g, sp, tw, ktab, blk);
 }
 
 // The packed block's last frames, one workgroup per frame, after k_cols.
@@ -1361,11 +1376,33 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, int f0, Geo g, Spec sp,
-                 const c2 *__restrict__ tw)
+                 const c2 *__restrict__ tw, const float2 *__restrict__ ktab)
 {
     const int fr = f0 + (int)blockIdx.x;   // >= 1
     k_cols_body<LOG2N, MODE, true>(G + (size_t)fr * g_stride, g_stride, G + (size_t)(fr - 1) * g_stride,
-                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, 0);
+                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, 0);
+}
+
+// K2's per-bin tables of every column in LDS slot order ([N/2+1][k2_tab_slots]):
+// the frame-invariant bin_static values (pyramid masks pre-scaled by inv_nn, a
+// power of two: exact), evaluated once per parameter set on the launch stream
+// (mm_api.hip launch_k2) instead of in every k_cols workgroup's prologue.
+template <int LOG2N, int MODE>
+__global__ __launch_bounds__(256) void k_k2_table(float2 *__restrict__ ktab, Spec sp)
+{
+    constexpr int N = 1 << LOG2N, TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
+    constexpr int C = fft_c_v(LOG2N), QN = k2_tab_q<LOG2N>();
+    const int id = blockIdx.x * 256 + threadIdx.x;
+    if (id >= (N / 2 + 1) * TS) return;
+    const int f = id / TS, slot = id - f * TS;
+    const int e = C == 1 ? slot : (slot % QN) * C + slot / QN;   // k2_tix(e) == slot
+    float2 v = make_float2(0.0f, 0.0f);
+    if (e < TE) {
+        const float ks = k2_tabled<MODE>() ? sp.inv_nn : 1.0f;
+        const float2 b = bin_static<LOG2N, MODE>(f, e, sp);
+        v = make_float2(b.x * ks, b.y * ks);
+    }
+    ktab[id] = v;
 }
 
 // =========================================================================

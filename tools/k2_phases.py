@@ -54,6 +54,15 @@ s0 = start - start.min()
 res["loop_start_skew_us"] = {q: round(float(np.percentile(s0, q)) / 100.0, 2) for q in (0, 50, 90, 100)}
 res["loop_duration_us"] = {q: round(float(np.percentile(dur, q)) / 1e3, 1) for q in (0, 50, 90, 100)}
 res["end_us_max"] = round(float((s0 * 10 + dur).max()) / 1e3, 1)
+if hasattr(L, "mm_debug_k2_entry"):   # kernel entry per wave (100 MHz): dispatch skew and prologue
+    eb = (ctypes.c_ulonglong * nw)()
+    L.mm_debug_k2_entry.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert L.mm_debug_k2_entry(eb, nw) == 0
+    ent = np.frombuffer(eb, dtype=np.uint64).astype(np.int64)
+    lo = ent & 0xffffffff
+    e0 = lo - lo.min()
+    res["entry_skew_us"] = {q: round(float(np.percentile(e0, q)) / 100.0, 2) for q in (0, 50, 90, 100)}
+    res["prologue_us"] = {q: round(float(np.percentile(start - lo, q)) / 100.0, 2) for q in (0, 50, 90, 100)}
 print(json.dumps(res))
 if len(sys.argv) > 2:
     np.save(sys.argv[2], raw)
