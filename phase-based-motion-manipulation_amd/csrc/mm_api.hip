@@ -781,6 +781,15 @@ static int compute_state(mm_handle *h, const uint8_t *in, int fmt, void *dst, hi
     return launch_k1<LOG2N>(h, in, 1, fmt, s, reinterpret_cast<c2 *>(dst));
 }
 
+// MM_ONLY_LOG2N=n (experiment builds only): instantiate one padded size, so an
+// A/B variant compiles in a fraction of the full build's time
+#ifdef MM_ONLY_LOG2N
+#define MM_DISPATCH(expr_template)                          \
+    switch (h->log2n) {                                     \
+    case MM_ONLY_LOG2N: return expr_template(MM_ONLY_LOG2N); \
+    default: return MM_ERR_UNSUPPORTED;                     \
+    }
+#else
 #define MM_DISPATCH(expr_template)                          \
     switch (h->log2n) {                                     \
     case 4: return expr_template(4);                        \
@@ -794,6 +803,7 @@ static int compute_state(mm_handle *h, const uint8_t *in, int fmt, void *dst, hi
     case 12: return expr_template(12);                      \
     default: return MM_ERR_UNSUPPORTED;                     \
     }
+#endif
 
 static int do_set_attrs(mm_handle *h)
 {
@@ -1060,7 +1070,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->yh_stride = (size_t)g.Hq * g.Wy;   // whole Q tiles of rows: K3 stores row pairs
 
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
         free_handle(h);
         return MM_ERR_HIP;
     }

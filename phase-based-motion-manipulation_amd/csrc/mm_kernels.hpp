@@ -152,6 +152,29 @@ __device__ __forceinline__ void st_off(void *base, unsigned byte_off, T v)
     *reinterpret_cast<T *>(reinterpret_cast<uint8_t *>(base) + byte_off) = v;
 }
 
+// Stores of whole 128-B lines that nothing reads back soon (output frames, Yh
+// rows): non-temporal, so that they stream out under the kernel instead of
+// sitting dirty in L2 for the write-back at the end of the kernel (same-call:
+// K34 -4 %, one-frame K3 / K4 -5 % / -7 %).  The partial-line hand-off stores
+// (G, Q) stay write-back: their pieces are merged in L2 (non-temporal there:
+// K1 3x, K2 1.8x slower, profiles/r03g_nt_ab.txt).
+template <class T>
+__device__ __forceinline__ void st_stream(void *base, unsigned byte_off, T v)
+{
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    void *p = reinterpret_cast<uint8_t *>(base) + byte_off;
+    if constexpr (sizeof(T) == 16) {
+        u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+    } else {
+        static_assert(sizeof(T) == 4, "st_stream: 4 or 16 bytes");
+        unsigned w;
+        __builtin_memcpy(&w, &v, 4);
+        __builtin_nontemporal_store(w, reinterpret_cast<unsigned *>(p));
+    }
+}
+
 // Q hand-off (K2 -> K3): element (row k, bin f) of a frame, stored in tiles of
 // TK rows: [k/TK][f][k%TK], Qs bins per tile row.  A K2 workgroup's columns of
 // one tile are contiguous (GPW*TK*8 bytes: whole 128-B lines at TK = 8), and
@@ -191,7 +214,7 @@ template <> struct Pix<0> {           // RGBA8 UNORM
     }
     __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
     {
-        st_off<uint32_t>(base, i * 4u, pack(r, g, b));
+        st_stream<uint32_t>(base, i * 4u, pack(r, g, b));
     }
 };
 template <> struct Pix<1> {           // RGBA32F
@@ -205,7 +228,7 @@ template <> struct Pix<1> {           // RGBA32F
     __device__ static float4 load(const uint8_t *base, size_t i) { return raw(base, i); }
     __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
     {
-        st_off<float4>(base, i * 16u, make_float4(r, g, b, 1.0f));
+        st_stream<float4>(base, i * 16u, make_float4(r, g, b, 1.0f));
     }
 };
 
@@ -716,6 +739,50 @@ __device__ __forceinline__ c2 pyramid_op_1band(c2 c, c2 p, const Spec &sp, float
     return mul(c, mk(mmag * cw + mpass, mmag * sw));
 }
 
+// pyramid_op_1band for two bins at once: the same operations, with the
+// atan2 polynomial, its reconstruction and the scale to revolutions of both
+// bins in packed FP32 (one v_pk_fma per step for two bins; v_pk_fma_f32 is a
+// fused multiply-add per half, so every value is the scalar form's bit for
+// bit).  Only the per-bin octant selects stay scalar (no abs modifier on
+// VOP3P sources).
+__device__ __forceinline__ void pyramid_op_1band_x2(c2 &v0, c2 &p0, float2 mt0, c2 &v1, c2 &p1, float2 mt1,
+                                                    const Spec &sp)
+{
+    const c2 c0 = v0, c1 = v1;
+    const float mn0 = fminf(c0.x * c0.x + c0.y * c0.y, p0.x * p0.x + p0.y * p0.y);
+    const float mn1 = fminf(c1.x * c1.x + c1.y * c1.y, p1.x * p1.x + p1.y * p1.y);
+    const float mmag0 = mt0.x * mt0.x * mn0 < sp.tau2_nn ? 0.0f : mt0.x;
+    const float mmag1 = mt1.x * mt1.x * mn1 < sp.tau2_nn ? 0.0f : mt1.x;
+    const float mpass0 = -mt0.y - mmag0, mpass1 = -mt1.y - mmag1;
+    const c2 u0 = mul_conj(p0, c0), u1 = mul_conj(p1, c1);
+    // octant reduction per bin (fast_atan2's expressions)
+    const float ax0 = fabsf(u0.x), ay0 = fabsf(u0.y), ax1 = fabsf(u1.x), ay1 = fabsf(u1.y);
+    const bool st0 = ay0 > ax0, st1 = ay1 > ax1;
+    const float a0 = (st0 ? ax0 : ay0) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(ax0, ay0), 1.17549435e-38f));
+    const float a1 = (st1 ? ax1 : ay1) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(ax1, ay1), 1.17549435e-38f));
+    const c2 a = mk(a0, a1), sq = a * a;
+    c2 r = mk(-0.00405455008149147f, -0.00405455008149147f);
+    r = r * sq + mk(0.021862903609871864f, 0.021862903609871864f);
+    r = r * sq - mk(0.055912263691425323f, 0.055912263691425323f);
+    r = r * sq + mk(0.09642193466424942f, 0.09642193466424942f);
+    r = r * sq - mk(0.1390862911939621f, 0.1390862911939621f);
+    r = r * sq + mk(0.19946566224098206f, 0.19946566224098206f);
+    r = r * sq - mk(0.33329859375953674f, 0.33329859375953674f);
+    r = r * sq + mk(0.9999993443489075f, 0.9999993443489075f);
+    const c2 ra = r * a;
+    const c2 rs = mk(1.57079632679489662f, 1.57079632679489662f) - ra;
+    float t0 = st0 ? rs.x : ra.x, t1 = st1 ? rs.y : ra.y;
+    if (u0.x < 0.0f) t0 = 3.14159265358979324f - t0;
+    if (u1.x < 0.0f) t1 = 3.14159265358979324f - t1;
+    const c2 rev = mk(copysignf(t0, u0.y), copysignf(t1, u1.y)) * mk(sp.S_rev, sp.S_rev);
+    const float cw0 = __builtin_amdgcn_cosf(rev.x), sw0 = __builtin_amdgcn_sinf(rev.x);
+    const float cw1 = __builtin_amdgcn_cosf(rev.y), sw1 = __builtin_amdgcn_sinf(rev.y);
+    v0 = mul(c0, mk(mmag0 * cw0 + mpass0, mmag0 * sw0));
+    v1 = mul(c1, mk(mmag1 * cw1 + mpass1, mmag1 * sw1));
+    p0 = c0;
+    p1 = c1;
+}
+
 // pyramid_op_1band in the power form (MM_K2_PYR_POW) for NB bins at once (their
 // squarings interleave): v[j] <- c w, prev[j] <- c for j = j0 .. j0 + NB - 1,
 // w = mpass + mmag z^S, the same gate and masks as pyramid_op_1band.
@@ -931,6 +998,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     c2 prev[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) prev[j] = mk(0.0f, 0.0f);
+
     // per-bin table bases of a regular group's bins (regular_op): bin j is
     // fy = fy0 + j N/8 (fy0 = fft_bin(t, 0)), table entry fy for j < 4, N - fy
     // for j >= 4; N/8 is a multiple of C, so both are slots of two
@@ -1139,6 +1207,18 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                 const int w = fy0 % C;
                 const float2 *tlo = HOIST ? tlo0 : tab0 + k2_tix<LOG2N>(fy0);
                 const float2 *thi = HOIST ? thi0 : tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
+#ifndef MM_K2_OPX1
+#pragma unroll
+#ifndef MM_K2_OPX2G
+#define MM_K2_OPX2G 2   // bins per scheduling group of the two-bin op
+#endif
+                for (int j = 0; j < 8; j += 2) {   // two bins per packed op
+                    if (j % MM_K2_OPX2G == 0) __builtin_amdgcn_sched_barrier(0);
+                    const float2 mt0 = j < 4 ? tlo[j * (N / 8) / C] : thi[(N - j * (N / 8)) / C];
+                    const float2 mt1 = j + 1 < 4 ? tlo[(j + 1) * (N / 8) / C] : thi[(N - (j + 1) * (N / 8)) / C];
+                    pyramid_op_1band_x2(v[j], prev[j], mt0, v[j + 1], prev[j + 1], mt1, sp);
+                }
+#else
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     if (j % MM_K2_OPG == 0) __builtin_amdgcn_sched_barrier(0);
@@ -1147,6 +1227,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     prev[j] = v[j];
                     v[j] = a;
                 }
+#endif
                 __builtin_amdgcn_sched_barrier(0);
             } else {
 #pragma unroll
@@ -1475,7 +1556,7 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
             o.y = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
             o.z = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
             o.w = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
-            *reinterpret_cast<float4 *>(out + (size_t)r * g.Wy + X) = o;
+            st_stream<float4>(out, (unsigned)((r * g.Wy + X) * 4), o);
         }
         return;
     }
@@ -1764,7 +1845,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
                         px.y = Pix<0>::pack(rr[1], gg[1], bb[1]);
                         px.z = Pix<0>::pack(rr[2], gg[2], bb[2]);
                         px.w = Pix<0>::pack(rr[3], gg[3], bb[3]);
-                        st_off<uint4>(outp, o * 4u, px);
+                        st_stream<uint4>(outp, o * 4u, px);
                     } else {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) Pix<1>::store(outp, o + k, rr[k], gg[k], bb[k]);
