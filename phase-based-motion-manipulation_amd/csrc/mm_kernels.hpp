@@ -1210,7 +1210,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #ifndef MM_K2_OPX1
 #pragma unroll
 #ifndef MM_K2_OPX2G
-#define MM_K2_OPX2G 2   // bins per scheduling group of the two-bin op
+#define MM_K2_OPX2G 8   // bins per scheduling group of the two-bin op (2, 4: K2 +3 %, +1 %)
 #endif
                 for (int j = 0; j < 8; j += 2) {   // two bins per packed op
                     if (j % MM_K2_OPX2G == 0) __builtin_amdgcn_sched_barrier(0);
