@@ -305,14 +305,43 @@ def parity_check(mm355, torch, params, W, H, ref, local):
             "bar": "max 1 LSB, <= 0.1% of values"}
 
 
+class _DevEvents:
+    """HIP events with a device-scope release (hipEventDisableSystemFence):
+    torch.cuda.Event records with a system-scope fence, a cache write-back per
+    record that would lengthen the one-frame calls it brackets."""
+    FLAGS = 0x20000000   # hipEventDisableSystemFence (hip_runtime_api.h)
+
+    def __init__(self, n):
+        import ctypes
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch and libmm355 share
+        self.ev = []
+        for _ in range(n):
+            e = ctypes.c_void_p()
+            assert self.hip.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(self.FLAGS)) == 0
+            self.ev.append(e)
+
+    def record(self, k, stream):
+        assert self.hip.hipEventRecord(self.ev[k], self.ct.c_void_p(stream)) == 0
+
+    def elapsed_ms(self, a, b):
+        ms = self.ct.c_float()
+        assert self.hip.hipEventElapsedTime(self.ct.byref(ms), self.ev[a], self.ev[b]) == 0
+        return ms.value
+
+    def close(self):
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+
+
 def drop_in_per_frame(mm355, torch, params, W, H, frames, local, count):
     """The reference's call pattern (OnRenderImage once per frame,
     .cs:101-143): a fresh handle at batch size 1, mm_process with device
     pointers, one frame per call on one stream.  Every call re-transforms the
     state G_{t-1} (K2's priming column FFT of the previous frame's row
-    spectra) and makes one launch per kernel.  Returns frames/s over the calls (after
-    the passthrough frame and 10 warm-up calls) and the HIP-event latency of
-    each call."""
+    spectra) and makes one launch per kernel.  frames/s: the calls alone
+    (wall clock, after the passthrough frame and 10 warm-up calls); latency:
+    a second pass with device-scope HIP events around each call."""
     h = mm355.Handle(W, H, params, device=local)
     h.set_batch(1)
     src = frames.reshape(-1, H, W, 4)
@@ -323,24 +352,28 @@ def drop_in_per_frame(mm355, torch, params, W, H, frames, local, count):
     count = min(count, src.shape[0] - warm)
     for k in range(warm):
         h.process(src[k], out[k & 1], mm355.RGBA8, on_device=True, stream=sp)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(count + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev[0].record(st)
     for k in range(count):
         h.process(src[warm + k], out[k & 1], mm355.RGBA8, on_device=True, stream=sp)
-        ev[k + 1].record(st)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    ev = _DevEvents(count + 1)
+    ev.record(0, sp)
+    for k in range(count):
+        h.process(src[warm + k], out[k & 1], mm355.RGBA8, on_device=True, stream=sp)
+        ev.record(k + 1, sp)
+    torch.cuda.synchronize()
+    lat = sorted(ev.elapsed_ms(k, k + 1) for k in range(count))
+    ev.close()
     h.close()
-    lat = sorted(ev[k].elapsed_time(ev[k + 1]) for k in range(count))
     pick = lambda q: round(lat[min(count - 1, int(q * count))], 5)
     return {"frames": count, "frames_per_s": round(count / wall, 2),
             "latency_ms": {"mean": round(sum(lat) / count, 5), "p50": pick(0.5),
                            "p99": pick(0.99), "max": round(lat[-1], 5)},
             "pattern": "mm_process(MM_FRAMES_ON_DEVICE), batch 1, one call per frame "
-                       "(.cs:101-143 OnRenderImage); latency = HIP events around each call "
-                       "on its stream"}
+                       "(.cs:101-143 OnRenderImage); frames/s = calls / wall time; latency = "
+                       "device-scope HIP events around each call on its stream (second pass)"}
 
 
 def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None, ran=None):

@@ -137,7 +137,10 @@ struct ProfScope {
         if (!on) return;
         r.kernel = kernel;
         r.frames = frames;
-        on = hipEventCreate(&r.a) == hipSuccess && hipEventCreate(&r.b) == hipSuccess &&
+        // timing only: a device-scope release (no system-scope cache write-back
+        // between the kernels being timed)
+        on = hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) == hipSuccess &&
+             hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) == hipSuccess &&
              hipEventRecord(r.a, s) == hipSuccess;
     }
     ~ProfScope()
