@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[1]): a synthetic 1920x1080 RGBA8 stream,
 5-level pyramid, PhaseScale 25, pyramid mode with orientations = 1 (the
 reference's semantics).  One STEP = one mm_process_stream call over the
 config's 300-frame stream per GPU (`--frames-per-step`), processed in batches
-of 100 frames (`--batch`, mm_set_batch).  Input frames are generated on the
+of 150 frames (`--batch`, mm_set_batch).  Input frames are generated on the
 device and resident in HBM before timing.
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): the stream is
@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--frames-per-step", type=int, default=300,
                     help="frames per step and GPU: one mm_process_stream call over the "
                          "config's 300-frame stream by default")
-    ap.add_argument("--batch", type=int, default=100,
+    ap.add_argument("--batch", type=int, default=150,
                     help="frames per K1/K2/K3/K4 batch inside a step (mm_set_batch; 0: the "
                          "whole step)")
     ap.add_argument("--width", type=int, default=1920)
