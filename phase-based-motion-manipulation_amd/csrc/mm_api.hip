@@ -73,6 +73,7 @@ struct mm_handle {
     size_t stage_bytes;
     bool has_state;
     int k2_tail_pct;            // share of a batch's frames of k_cols's packed block run by k_cols_tail
+    int k2_tail2_pct;           // share of the second-half blocks' frames run by k_cols's tail blocks
     int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused;
                                 // -1: by the launch's frame count, k34_strip_rows)
     // mm_profile_begin/end: HIP events around each launch on its stream
@@ -405,11 +406,15 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
     // the packed block's last k frames go to k_cols_tail (k_cols's critical path)
     int k = nframes >= 24 ? nframes * h->k2_tail_pct / 100 : 0;
     k = std::max(0, std::min(k, nframes - 2));
+    // second-half tails (k_cols): the last k2 frames of each second-half block's
+    // columns in extra blocks (MM_K2_TAIL2 percent)
+    const int k2t = nframes >= 24 && blocks >= 2 ? std::min(nframes * h->k2_tail2_pct / 100, nframes - 2) : 0;
+    const int tb = k2t > 0 ? blocks / 2 : 0;
 #define MM_K2_LAUNCH(MODE)                                                                           \
     do {                                                                                             \
-        hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks), dim3(k2_threads<LOG2N>()), lds, s, G, \
+        hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks + tb), dim3(k2_threads<LOG2N>()), lds, s, G, \
                            h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, h->d_ktab, \
-                           nframes - k);                                                             \
+                           nframes - k, tb, k2t);                                                    \
         if (k)                                                                                       \
             hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G, \
                                h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab); \
@@ -1065,6 +1070,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
+    h->k2_tail2_pct = getenv("MM_K2_TAIL2") ? atoi(getenv("MM_K2_TAIL2")) : 10;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
 
     h->chunk = default_batch(width, height, N);

@@ -935,7 +935,7 @@ template <int LOG2N, int MODE, bool BLK0>
 __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q,
                                             size_t q_stride, int nframes, const Geo &g,
                                             const Spec &sp, const c2 *__restrict__ tw,
-                                            const float2 *__restrict__ ktab, int blk)
+                                            const float2 *__restrict__ ktab, int blk, int nb_prio = 0)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     constexpr int TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
@@ -1097,7 +1097,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         // path, phase stamps) keeps the highest priority throughout (same-call
         // A/B: ≈ 1 % over alternating it too, and over raising the packed group only).
         if (blk0) __builtin_amdgcn_s_setprio(3);
-        else if ((fr ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
+        else if ((fr ^ ((int)blockIdx.x >= nb_prio / 2 ? 1 : 0)) & 1) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
 #ifdef MM_K2_NOGAHEAD
         load_g(fr < nframes ? fr : nframes - 1, t);
@@ -1434,15 +1434,30 @@ template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
             int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, const float2 *__restrict__ ktab,
-            int nframes_blk0)
+            int nframes_blk0, int tail_blocks, int ktail)
 {
+    // Blocks nb .. nb + tail_blocks - 1 (tail_blocks <= nb / 2) are tails: the
+    // last ktail frames of the columns of second-half block nb/2 + i, which
+    // stops that many frames early.  A CU's second workgroup (the younger,
+    // second half of the dispatch) runs behind its first all launch long
+    // (phase stamps: first half done at ~825 us, second at ~1,045 us per 100
+    // frames); its tail starts in the slot the first one frees, primed with the
+    // frame before its first (the state is a pure function of that frame).
+    const int nb = gridDim.x - tail_blocks;
+    const bool tail = (int)blockIdx.x >= nb;
+    const int p = tail ? nb / 2 + ((int)blockIdx.x - nb) : (int)blockIdx.x;
     // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
     // are merged in one L2 (split over XCDs they left as partial-line writes)
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    if (blk == 0)   // the packed block stops nframes_blk0 frames in (k_cols_tail)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, blk);
-    else
-        k_cols_body<LOG2N, MODE, false>(G, g_stride, Gprev, Q, q_stride, nframes, g, sp, tw, ktab, blk);
+    const int blk = xcd_remap(p, nb);
+    if (blk == 0) {   // the packed block stops nframes_blk0 frames in (k_cols_tail)
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, blk, nb);
+    } else {
+        const int f0 = tail ? nframes - ktail : 0;
+        const int nf = tail ? ktail : (p >= nb / 2 && p - nb / 2 < tail_blocks ? nframes - ktail : nframes);
+        k_cols_body<LOG2N, MODE, false>(G + (size_t)f0 * g_stride, g_stride,
+                                        tail ? G + (size_t)(f0 - 1) * g_stride : Gprev,
+                                        Q + (size_t)f0 * q_stride, q_stride, nf, g, sp, tw, ktab, blk, nb);
+    }
 }
 
 // The packed block's last frames, one workgroup per frame, after k_cols.

@@ -257,3 +257,34 @@ def test_refused_geometries():
         with pytest.raises(mm355.MMError) as ei:
             mm355.Handle(W, H)
         assert ei.value.code == -2, (W, H)
+
+
+@pytest.mark.parametrize("W,H,n", [(1920, 1080, 30), (640, 360, 48)])
+def test_k2_second_half_tails_bitwise(W, H, n):
+    """k_cols's tail blocks (MM_K2_TAIL2 percent of the second-half blocks'
+    frames, each primed with the frame before its first) give the same bits as
+    no tails and as a larger share."""
+    import os
+    import torch
+    import mm355
+    fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    outs = []
+    for pct in ("0", "10", "40"):
+        old = os.environ.get("MM_K2_TAIL2")
+        os.environ["MM_K2_TAIL2"] = pct
+        try:
+            h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
+        finally:
+            if old is None:
+                del os.environ["MM_K2_TAIL2"]
+            else:
+                os.environ["MM_K2_TAIL2"] = old
+        h.set_batch(n)
+        if not outs:
+            h.synth(fr, 0, n)
+        o = torch.empty_like(fr)
+        h.process_stream(fr, o, n, mm355.RGBA8)
+        torch.cuda.synchronize()
+        h.close()
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
