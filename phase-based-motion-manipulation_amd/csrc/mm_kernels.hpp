@@ -960,6 +960,45 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     constexpr bool blk0 = BLK0;               // block 0 runs the extra exchanges
     const bool packed = blk0 && grp == 0;     // group owning columns 0 and N/2
 
+    // G column of a frame.  Rows outside the image get an out-of-range buffer
+    // offset: the range check returns 0 for them without a memory access (the
+    // zero padding of PadTexture, .cs:358-381).  A frame's loads are issued
+    // before the previous frame's Q stores, so the wait for them never waits
+    // for those stores (one in-order vmcnt).  (Loading one frame ahead, 16
+    // more VGPRs, measured no faster: the frame loop is bound by its barrier
+    // and dependency-chain latencies, not by this load's.)
+    c2 ga[8];
+    float gb[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    // (buffer loads: 32-bit offsets, and kept in order with the buffer stores)
+    // One buffer resource per column, its range the H image rows: row t + jT - y0
+    // at byte offset (t - y0) 8 + j T 8, and rows outside the image (negative
+    // offsets wrap to huge ones) fail the range check without any compare.
+    auto load_g = [&](int fr, int t) {
+        const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform; -1: Gprev
+        const c2 *Gc = gfr < 0 ? Gprev : G + (size_t)gfr * g_stride;
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)f * g.Hg, 0,
+                                                           g.H * (int)sizeof(c2), 0x00020000);
+        const unsigned o0 = (unsigned)(t - g.y0) * 8u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, o0 + (unsigned)(j * T * 8), 0, 0);
+            ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
+        }
+        if constexpr (blk0) {   // column N/2 (real) for the packed group's block only
+            const auto nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)(N / 2) * g.Hg, 0,
+                                                               g.H * (int)sizeof(c2), 0x00020000);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, o0 + (unsigned)(j * T * 8), 0, 0));
+        }
+    };
+#ifndef MM_K2_NOGAHEAD
+    // the prime's G_{t-1} loads first: their HBM latency overlaps the twiddle
+    // loads and the table copy instead of following its barrier (one-frame
+    // calls pay the prologue and the prime on every call)
+    load_g(-1, t0);
+#endif
     // twiddle bases of both FFTs, loaded once (issued under the table copy): no loads inside a frame but G's
     c2 wtw[16];
 #pragma unroll
@@ -1013,39 +1052,6 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     const float2 *tlo0 = tab0 + k2_tix<LOG2N>(hfy0);
     const float2 *thi0 = tab0 + (hw ? k2_tix<LOG2N>(fft_c_v(LOG2N) - hw) - 1 : 0) - hfy0 / fft_c_v(LOG2N);
 
-    // G column of a frame.  Rows outside the image get an out-of-range buffer
-    // offset: the range check returns 0 for them without a memory access (the
-    // zero padding of PadTexture, .cs:358-381).  A frame's loads are issued
-    // before the previous frame's Q stores, so the wait for them never waits
-    // for those stores (one in-order vmcnt).  (Loading one frame ahead, 16
-    // more VGPRs, measured no faster: the frame loop is bound by its barrier
-    // and dependency-chain latencies, not by this load's.)
-    c2 ga[8];
-    float gb[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    // (buffer loads: 32-bit offsets, and kept in order with the buffer stores)
-    // One buffer resource per column, its range the H image rows: row t + jT - y0
-    // at byte offset (t - y0) 8 + j T 8, and rows outside the image (negative
-    // offsets wrap to huge ones) fail the range check without any compare.
-    auto load_g = [&](int fr, int t) {
-        const int gfr = __builtin_amdgcn_readfirstlane(fr);   // uniform; -1: Gprev
-        const c2 *Gc = gfr < 0 ? Gprev : G + (size_t)gfr * g_stride;
-        const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)f * g.Hg, 0,
-                                                           g.H * (int)sizeof(c2), 0x00020000);
-        const unsigned o0 = (unsigned)(t - g.y0) * 8u;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(grs, o0 + (unsigned)(j * T * 8), 0, 0);
-            ga[j] = mk(__uint_as_float(a.x), __uint_as_float(a.y));
-        }
-        if constexpr (blk0) {   // column N/2 (real) for the packed group's block only
-            const auto nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2 *>(Gc) + (size_t)(N / 2) * g.Hg, 0,
-                                                               g.H * (int)sizeof(c2), 0x00020000);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                gb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, o0 + (unsigned)(j * T * 8), 0, 0));
-        }
-    };
     constexpr int TK = q_tile<LOG2N>(), BLK = GPW * TK / 2;   // float4 per tile row
     constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
     const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
@@ -1102,7 +1108,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #ifdef MM_K2_NOGAHEAD
         load_g(fr < nframes ? fr : nframes - 1, t);
 #else
-        if (fr < 0) load_g(-1, t);   // Gprev; later frames' loads were issued mid-iteration
+        // (Gprev: issued before the prologue; later frames' loads mid-iteration)
 #endif
         K2_STAMP(0);
         __builtin_amdgcn_sched_barrier(0);   // keep the stores behind the loads

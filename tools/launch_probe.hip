@@ -66,5 +66,27 @@ int main()
             if (pass) printf("{\"kernel\": \"%s\", \"us_per_launch\": %.2f}\n", nm[v], ms * 1e3 / R);
         }
     }
+    // the same 200 empty 512x512 launches captured once into a hipGraph and
+    // replayed: per-node cost of graph dispatch against stream launches
+    {
+        hipStream_t cs;
+        CHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        hipGraph_t gr;
+        hipGraphExec_t ge;
+        CHK(hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal));
+        for (int r = 0; r < R; ++r) hipLaunchKernelGGL(k_empty, dim3(512), dim3(512), 0, cs, flag);
+        CHK(hipStreamEndCapture(cs, &gr));
+        CHK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+        for (int pass = 0; pass < 2; ++pass) {
+            CHK(hipStreamSynchronize(cs));
+            CHK(hipEventRecord(e0, cs));
+            CHK(hipGraphLaunch(ge, cs));
+            CHK(hipEventRecord(e1, cs));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            if (pass) printf("{\"kernel\": \"graph of 200 empty 512x512\", \"us_per_launch\": %.2f}\n", ms * 1e3 / R);
+        }
+    }
     return 0;
 }
