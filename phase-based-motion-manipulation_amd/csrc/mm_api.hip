@@ -358,6 +358,9 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
     do {                                                                                           \
         constexpr int gpw = k1_gpw<LOG2N, LAT>();                                                  \
         const size_t lds = sizeof(c2) * (size_t)gpw * lds_complex<(1 << LOG2N)>();                \
+        if (lds > 65536)                                                                           \
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_fwd<LOG2N, F, GEN, LAT>), \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
         hipLaunchKernelGGL((k_rows_fwd<LOG2N, F, GEN, LAT>), dim3((total + gpw - 1) / gpw),         \
                            dim3(gpw * fft_T<LOG2N>()), lds, s, in, fb, ppf, total, h->geo,         \
                            h->d_col3, h->d_row3, h->d_col, h->d_row, h->d_tw, G, h->g_stride);     \
