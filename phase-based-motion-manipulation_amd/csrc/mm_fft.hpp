@@ -164,6 +164,21 @@ __device__ __forceinline__ void apply_twiddles(c2 *u, c2 w1)
     }
 }
 
+// The same multiplies with the powers w^1 .. w^7 of one radix-8 pass read from
+// an LDS table (tw_tab_build: identical products, so identical values):
+// p[k NS] holds (w^{2k+1}, w^{2k+2}), k = 0..3 (the last .zw unused).
+template <int DIR, int NS>
+__device__ __forceinline__ void apply_twiddles_tt(c2 *u, const float4 *p)
+{
+    const float4 a = p[0], b = p[NS], c = p[2 * NS], d = p[3 * NS];
+    u[1] = mul_tw<DIR>(u[1], mk(a.x, a.y));
+    u[2] = mul_tw<DIR>(u[2], mk(a.z, a.w));
+    u[3] = mul_tw<DIR>(u[3], mk(b.x, b.y));
+    u[4] = mul_tw<DIR>(u[4], mk(b.z, b.w));
+    u[5] = mul_tw<DIR>(u[5], mk(c.x, c.y));
+    u[6] = mul_tw<DIR>(u[6], mk(c.z, c.w));
+    u[7] = mul_tw<DIR>(u[7], mk(d.x, d.y));
+}
 
 constexpr int fft_passes_v(int log2n) { return log2n / 3 + (log2n % 3 ? 1 : 0); }
 template <int LOG2N> constexpr int fft_passes() { return fft_passes_v(LOG2N); }
@@ -211,6 +226,30 @@ constexpr int xpad_a(int log2n, int ns) { return log2n < 9 || ns == 1 ? 1 : (ns 
 template <int LOG2N, int NS>
 __host__ __device__ constexpr int xpad(int i) { return i + xpad_a(LOG2N, NS) * (i >> xpad_s(LOG2N, NS)); }
 
+// Twiddle-power table of the inner 512-point transform (passes 1 and 2, radix
+// 8, NS = 8 and 64): pass P's powers of base index i at tt[tw_tab_off(P) +
+// k NS + i], k = 0..3 (float4 = two powers).  4.5 KB of LDS.
+__host__ __device__ constexpr int tw_tab_off(int p) { return p == 1 ? 0 : 4 * 8; }
+constexpr int tw_tab_float4() { return 4 * 8 + 4 * 64; }
+// Fills the table: entry i < 8 is pass 1's base W_64^i, i >= 8 pass 2's
+// W_512^(i-8), read from the W_N table at stride C (preload_twiddles_wl's
+// bases) and raised with apply_twiddles' exact products.  Threads tid of nthr.
+__device__ __forceinline__ void tw_tab_build(float4 *tt, int tid, int nthr, const c2 *__restrict__ tw, int C)
+{
+    for (int e = tid; e < 8 + 64; e += nthr) {
+        const bool p1 = e < 8;
+        const int i = p1 ? e : e - 8, ns = p1 ? 8 : 64;
+        const c2 w1 = tw[(p1 ? i * 8 : i) * C];
+        const c2 w2 = mul(w1, w1), w3 = mul(w2, w1), w4 = mul(w2, w2);
+        const c2 w5 = mul(w1, w4), w6 = mul(w2, w4), w7 = mul(w3, w4);
+        float4 *o = tt + (p1 ? tw_tab_off(1) : tw_tab_off(2)) + i;
+        o[0] = make_float4(w1.x, w1.y, w2.x, w2.y);
+        o[ns] = make_float4(w3.x, w3.y, w4.x, w4.y);
+        o[2 * ns] = make_float4(w5.x, w5.y, w6.x, w6.y);
+        o[3 * ns] = make_float4(w7.x, w7.y, 0.0f, 0.0f);
+    }
+}
+
 // One Stockham pass (radix R, stride Ns).  B = 8/R butterflies per thread;
 // butterfly b = t + q*T reads x[b + m*N/R] (= register q + m*B) and writes
 // y[(b/Ns)*Ns*R + b%Ns + m*Ns].
@@ -225,8 +264,11 @@ __device__ __forceinline__ void xsync()
     else __syncthreads();
 }
 
-template <int LOG2N, int P, int DIR, bool WSYNC = false>
-__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+// TT: the pass's twiddle powers come from the LDS table tt (tw_tab_build)
+// instead of products of the base wb[P*4 + q]
+template <int LOG2N, int P, int DIR, bool WSYNC = false, bool TT = false>
+__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+                                         const float4 *tt = nullptr)
 {
     constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
     constexpr int NS = pass_ns_v(LOG2N, P);
@@ -237,7 +279,10 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
         c2 u[R];
 #pragma unroll
         for (int m = 0; m < R; ++m) u[m] = v[q + m * B];
-        if constexpr (NS > 1) apply_twiddles<R, DIR>(u, wb[P * 4 + q]);
+        if constexpr (NS > 1) {
+            if constexpr (TT && R == 8) apply_twiddles_tt<DIR, NS>(u, tt + tw_tab_off(P) + (b & (NS - 1)));
+            else apply_twiddles<R, DIR>(u, wb[P * 4 + q]);
+        }
         if constexpr (R == 8) dft8<DIR>(u);
         else if constexpr (R == 4) dft4<DIR>(u[0], u[1], u[2], u[3]);
         else dft2<DIR>(u[0], u[1]);
@@ -265,12 +310,13 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
     }
 }
 
-template <int LOG2N, int DIR, int P, bool WSYNC = false>
-__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+template <int LOG2N, int DIR, int P, bool WSYNC = false, bool TT = false>
+__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+                                              const float4 *tt = nullptr)
 {
     if constexpr (P < fft_passes<LOG2N>()) {
-        fft_pass<LOG2N, P, DIR, WSYNC>(v, t, lds, wb);
-        fft_pass_loop<LOG2N, DIR, P + 1, WSYNC>(v, t, lds, wb);
+        fft_pass<LOG2N, P, DIR, WSYNC, TT>(v, t, lds, wb, tt);
+        fft_pass_loop<LOG2N, DIR, P + 1, WSYNC, TT>(v, t, lds, wb, tt);
     }
 }
 
@@ -386,8 +432,9 @@ __device__ __forceinline__ void dft_c(c2 *u)
     else dft2<DIR>(u[0], u[1]);
 }
 
-template <int LOG2N, int DIR>
-__device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+template <int LOG2N, int DIR, bool TT = false>
+__device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+                                        const float4 *tt = nullptr)
 {
     constexpr int C = fft_c_v(LOG2N), H = 8 / C, RS = fft_region_v(LOG2N);
     if constexpr (C == 1) {
@@ -410,12 +457,13 @@ __device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&w
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = reg[l + 64 * j];
         __builtin_amdgcn_wave_barrier();
-        fft_pass_loop<9, DIR, 0, true>(v, l, reg, wb);
+        fft_pass_loop<9, DIR, 0, true, TT>(v, l, reg, wb, tt);
     }
 }
 
-template <int LOG2N, int DIR>
-__device__ __forceinline__ void fft_dit(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16])
+template <int LOG2N, int DIR, bool TT = false>
+__device__ __forceinline__ void fft_dit(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+                                        const float4 *tt = nullptr)
 {
     constexpr int C = fft_c_v(LOG2N), H = 8 / C, RS = fft_region_v(LOG2N);
     if constexpr (C == 1) {
@@ -423,7 +471,7 @@ __device__ __forceinline__ void fft_dit(c2 (&v)[8], int t, c2 *lds, const c2 (&w
     } else {
         const int w = t >> 6, l = t & 63;
         c2 *reg = lds + w * RS;
-        fft_pass_loop<9, DIR, 0, true>(v, l, reg, wb);   // over k2 -> n2, region w
+        fft_pass_loop<9, DIR, 0, true, TT>(v, l, reg, wb, tt);   // over k2 -> n2, region w
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < 8; ++j) reg[l + 64 * j] = v[j];

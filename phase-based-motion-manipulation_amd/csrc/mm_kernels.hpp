@@ -884,11 +884,21 @@ template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * ff
 // per-bin table, plus for column N/2 (packed group only) its table, its
 // previous spectrum (bins 0..N/2) and its staged Q values (one float per row).
 // Above 64 KiB at N = 2048 (77.8 KiB): two workgroups still fit a CU's 160 KiB.
+// The inner 512-point passes of k_cols's column FFTs take their twiddle
+// powers from an LDS table (tw_tab_build) instead of 6 products per pass
+// (MM_K2_TWTAB=1; default 0: same-call K2 8.08 -> 8.21 us/frame with the
+// table, profiles/r03k_k2_twtab_ab.txt: the LDS reads cost more than the
+// 48 VALU products per wave-frame they replace)
+#ifndef MM_K2_TWTAB
+#define MM_K2_TWTAB 0
+#endif
+template <int LOG2N> constexpr bool k2_twtab() { return MM_K2_TWTAB && fft_c_v(LOG2N) > 1; }
 template <int LOG2N> constexpr size_t k2_lds_bytes()
 {
     return (size_t)k2_groups<LOG2N>() *
                (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_slots<LOG2N>()) +
-           sizeof(float2) * k2_tab_slots<LOG2N>() + sizeof(c2) * 4 + sizeof(float) * (1 << LOG2N);
+           sizeof(float2) * k2_tab_slots<LOG2N>() + sizeof(c2) * 4 + sizeof(float) * (1 << LOG2N) +
+           (k2_twtab<LOG2N>() ? sizeof(float4) * tw_tab_float4() : 0);
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
@@ -1000,10 +1010,19 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     load_g(-1, t0);
 #endif
     // twiddle bases of both FFTs, loaded once (issued under the table copy): no loads inside a frame but G's
+    constexpr bool TT = k2_twtab<LOG2N>();
+    float4 *ttab = reinterpret_cast<float4 *>(stgN + N);   // inner passes' twiddle powers (TT)
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles_wl<LOG2N>(wtw, t0, tw);
+    if constexpr (TT) {   // outer-stage bases only; the inner passes read ttab
+#pragma unroll
+        for (int h = 0; h < 8 / fft_c_v(LOG2N); ++h) wtw[12 + h] = tw[t0 + 64 * fft_c_v(LOG2N) * h];
+        tw_tab_build(ttab, threadIdx.x, GPW * T, tw, fft_c_v(LOG2N));
+        if constexpr (MODE == MM_MODE_PYRAMID) __syncthreads();
+    } else {
+        preload_twiddles_wl<LOG2N>(wtw, t0, tw);
+    }
     if constexpr (MODE != MM_MODE_PYRAMID) {
         // the column's table, evaluated once per parameter set by k_k2_table
         // (slot order): a copy instead of N/2+1 bin_static per group and launch
@@ -1165,11 +1184,11 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             wt[i] = wtw[i];
-            if (tw_slot_used_wl(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
+            if (tw_slot_used_wl(LOG2N, i) && !(TT && i < 12)) asm volatile("" : "+v"(wt[i]));
         }
         K2_STAMP(2);
         MM_MARK("M1_fwd_start");
-        fft_dif<LOG2N, -1>(v, t, lds, wt);
+        fft_dif<LOG2N, -1, TT>(v, t, lds, wt, ttab);
         MM_MARK("M2_fwd_end");
         K2_STAMP(3);
         const bool pass_frame = fr < 0;
@@ -1365,7 +1384,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         if (!pass_frame) {
         K2_STAMP(4);
         MM_MARK("M3_inv_start");
-        fft_dit<LOG2N, +1>(v, t, lds, wt);   // natural row order again
+        fft_dit<LOG2N, +1, TT>(v, t, lds, wt, ttab);   // natural row order again
         MM_MARK("M4_inv_end");
         K2_STAMP(5);
         __syncthreads();   // every wave past its exchange reads: the staging overwrites them
