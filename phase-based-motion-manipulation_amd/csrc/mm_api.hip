@@ -76,6 +76,9 @@ struct mm_handle {
     int k2_tail2_pct;           // share of the second-half blocks' frames run by k_cols's tail blocks
     int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused;
                                 // -1: by the launch's frame count, k34_strip_rows)
+    int k34_oneshot;            // short launches: k_rows_inv_compose4 when its strips fit one
+                                // workgroup round (MM_K34_ONESHOT: 0 never: K3 -> K4, 2 always)
+    int num_cu;                 // compute units of the device
     // mm_profile_begin/end: HIP events around each launch on its stream
     struct ProfRec { hipEvent_t a, b; int kernel, frames; };
     bool prof;
@@ -342,6 +345,13 @@ static int set_attrs(int W)
         HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, 1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     }
+    if constexpr (LOG2N == 11) {   // k_rows_inv_compose4: four 2048-point groups, 73.7 KB
+        const int lds = (int)(sizeof(c2) * 4 * lds_complex<2048>());
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose4<11, 0>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose4<11, 1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    }
     return MM_OK;
 }
 
@@ -509,6 +519,32 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     if (nout <= 0) return MM_OK;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
     const int R = k34_strip_rows(h, nout);
+    // Short launches (the one-frame call) at N <= 1024 whose strips fit one
+    // workgroup round (4 waves per SIMD at <= 128 VGPRs: 1024 / 4T workgroups
+    // per CU): K3 + K4 fused in one shot, four FFT groups per 4-row strip, no
+    // walk (k_rows_inv_compose4).  One-frame calls, same call
+    // (profiles/r03k_k34_oneshot.txt): 960x540 33.0 -> 29.8 us, 640x480
+    // 30.4 -> 28.3 us, 1024x768 equal; at N = 2048 (16-wave workgroups, one
+    // per CU) it lost even in one round (1280x720 42.0 -> 42.6 us) and 1080p's
+    // 270 strips take two rounds (48.0 -> 54.4 us): K3 -> K4 there
+    // (MM_K34_ONESHOT=2 forces it, 0 disables it).
+    constexpr int k34o_per_cu = 4 * fft_T<LOG2N>() <= 1024 ? 1024 / (4 * fft_T<LOG2N>()) : 0;
+    if constexpr (LOG2N <= 11) if (R == 0 && h->k34_rows < 0 && h->k34_oneshot && k34_fits(h) &&
+                                   ((LOG2N <= 10 && (h->H + 3) / 4 * nout <= k34o_per_cu * h->num_cu) ||
+                                    h->k34_oneshot == 2)) {
+        const int strips = (h->H + 3) / 4;
+        const size_t lds = sizeof(c2) * 4 * lds_complex<(1 << LOG2N)>();
+        const dim3 grid((unsigned)(strips * nout)), block(4 * fft_T<LOG2N>());
+        ProfScope ps(h, s, MM_K_ROWS_INV_COMPOSE, nout);
+        if (fmt == MM_RGBA8)
+            hipLaunchKernelGGL((k_rows_inv_compose4<LOG2N, 0>), grid, block, lds, s, h->d_Q, h->q_stride,
+                               in, out, fb, frame0, strips, h->geo, h->blur, h->d_col3, h->d_row3, h->d_tw);
+        else
+            hipLaunchKernelGGL((k_rows_inv_compose4<LOG2N, 1>), grid, block, lds, s, h->d_Q, h->q_stride,
+                               in, out, fb, frame0, strips, h->geo, h->blur, h->d_col3, h->d_row3, h->d_tw);
+        HIPCHK(hipGetLastError());
+        return MM_OK;
+    }
     if (R >= 4 && k34_fits(h)) {   // K3 + K4 fused: Yh stays on chip
         const int strips = (h->H + R - 1) / R, steps = R / 4 + 1;
         const size_t lds = sizeof(c2) * 2 * lds_complex<(1 << LOG2N)>();
@@ -1050,6 +1086,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->log2n = 0;
     while ((1 << h->log2n) < N) ++h->log2n;
     h->device = hip_device;
+    h->num_cu = prop.multiProcessorCount;
     h->p = *p;
     Geo &g = h->geo;
     g.W = width;
@@ -1075,6 +1112,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
     h->k2_tail2_pct = getenv("MM_K2_TAIL2") ? atoi(getenv("MM_K2_TAIL2")) : 10;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
+    h->k34_oneshot = getenv("MM_K34_ONESHOT") ? atoi(getenv("MM_K34_ONESHOT")) : 1;
 
     h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * g.Hg;

@@ -1915,6 +1915,147 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
 #endif
 }
 
+// K34 in one shot, for short launches (the one-frame drop-in call): a strip of
+// 4 output rows needs list rows i0 .. i0+7, so a workgroup of FOUR FFT groups
+// transforms all of them at once (group g: list-row pair i0/2 + g, exactly
+// k_rows_inv_compose's step code), and then its two halves compose output
+// rows i0 + 2hh and i0 + 2hh + 1 (hh = 0, 1) from the 6 list rows and 4 source
+// rows they read: no sequential walk.  Twice the FFTs of the walking form
+// (every list row is transformed by two strips), but one workgroup round, one
+// launch instead of K3 + K4, and no Yh round trip.  Same expressions in the
+// same order as K3 + K4: bitwise equal (tests/test_k34.py).  N <= 2048 (4T
+// threads <= 1024).
+template <int LOG2N, int FMT>
+__global__ __launch_bounds__(4 * fft_T<LOG2N>())
+void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
+                         const uint8_t *__restrict__ frames_in, uint8_t *__restrict__ frames_out,
+                         size_t frame_bytes, int frame0, int strips, Geo g, Blur5 bw,
+                         const float4 *__restrict__ colW3, const float4 *__restrict__ rowW3,
+                         const c2 *__restrict__ tw)
+{
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), TK = q_tile<LOG2N>();
+    using raw_t = typename Pix<FMT>::raw_t;
+    constexpr unsigned bpp = Pix<FMT>::bpp;
+    extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
+    const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
+    const int t = threadIdx.x % T;
+    c2 *lds = lds_all + grp * lds_complex<N>();
+    const float *raw_all = reinterpret_cast<const float *>(lds_all);
+    constexpr int GROUP_FLOATS = 2 * lds_complex<N>();
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int frame = frame0 + b / strips;
+    const int i0 = (b % strips) * 4;
+    const c2 *Qf = Q + (size_t)frame * q_stride;
+    const uint8_t *img = frames_in + (size_t)frame * frame_bytes;
+    uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
+
+    // ---- K3 on list-row pair i0/2 + grp (zero beyond Hn) ----
+    {
+        const int ka = i0 + 2 * grp;
+        const bool valid = ka < g.Hn;
+        const int kl = valid ? ka : 0;
+        const float4 *Qp = reinterpret_cast<const float4 *>(Qf + (size_t)(kl / TK) * g.Qs * TK + (kl % TK));
+        float4 qv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int fq = t + j * T;
+            const int ff = fq > N / 2 ? N - fq : fq;
+            qv[j] = Qp[(size_t)ff * (TK / 2)];
+        }
+        c2 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int fq = t + j * T;
+            const bool mirror = fq > N / 2;
+            const int ff = mirror ? N - fq : fq;
+            float4 qq = qv[j];
+            if (ff == 0 || ff == N / 2) { qq.y = 0.0f; qq.w = 0.0f; }
+            if (mirror) { qq.y = -qq.y; qq.w = -qq.w; }
+            v[j] = valid ? mk(qq.x - qq.w, qq.y + qq.z) : mk(0.0f, 0.0f);
+        }
+        fft_regs<LOG2N, +1>(v, t, lds, tw);
+        float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows ka, ka+1
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            raw[t + j * T] = fabsf(v[j].x);
+            raw[N + t + j * T] = fabsf(v[j].y);
+        }
+    }
+    __syncthreads();
+
+    // ---- compose: half hh of the workgroup, output rows i0 + 2hh, i0 + 2hh + 1 ----
+    const int q = threadIdx.x % (2 * T), hh = threadIdx.x / (2 * T);
+    const bool vq = 4 * q < g.W;
+    const int X = vq ? 4 * q : g.W - 4;
+    const unsigned cl = (unsigned)wrap_near(X - 1, g.W, g.edge);
+    const unsigned cr = (unsigned)wrap_near(X + 4, g.W, g.edge);
+    auto chroma_row = [&](int i, c2 (&hc)[4]) {   // k_rows_inv_compose's
+        const int row = wrap_near(min(i, g.H), g.H, g.edge);
+        const unsigned base = (unsigned)(row * g.W);
+        raw_t p[6];
+        p[0] = ld_off<raw_t>(img, (base + cl) * bpp);
+        if constexpr (FMT == 0) {
+            const uint4 m = ld_off<uint4>(img, (base + (unsigned)X) * bpp);
+            p[1] = m.x; p[2] = m.y; p[3] = m.z; p[4] = m.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) p[1 + k] = ld_off<raw_t>(img, (base + (unsigned)X + k) * bpp);
+        }
+        p[5] = ld_off<raw_t>(img, (base + cr) * bpp);
+        c2 a[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[k] = chroma_iq2<FMT>(p[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 wc = colW3[X + k];
+            hc[k] = wc.x * a[k] + wc.y * a[k + 1] + wc.z * a[k + 2];
+        }
+    };
+    const int r0 = i0 + 2 * hh;   // first output row of this half
+    c2 hc[4][4];                  // combined (I, Q) of source rows r0-1 .. r0+2
+#pragma unroll
+    for (int k = 0; k < 4; ++k) chroma_row(r0 - 1 + k, hc[k]);
+    float yw[6][4];               // list rows r0 .. r0+5 of the quad, blurred horizontally
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int r = 2 * hh + k;   // list row i0 + r: group r/2, row r%2
+        const float *rw = raw_all + (r >> 1) * GROUP_FLOATS + (r & 1) * N + g.x0 + X;
+        const float4 *r4 = reinterpret_cast<const float4 *>(rw);
+        const float4 A = r4[-1], B = r4[0], C = r4[1];
+        yw[k][0] = bw.w0 * B.x + bw.w1 * (A.w + B.y) + bw.w2 * (A.z + B.z);
+        yw[k][1] = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
+        yw[k][2] = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
+        yw[k][3] = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int i = r0 + r;
+        if (vq && i < g.H) {
+            const float4 wr = rowW3[i];
+            float rr[4], gg[4], bb[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const c2 cc = wr.x * hc[r][k] + wr.y * hc[r + 1][k] + wr.z * hc[r + 2][k];
+                const float yb = bw.w0 * yw[r + 2][k] + bw.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
+                                 bw.w2 * (yw[r][k] + yw[r + 4][k]);
+                yiq_rgb(yb, cc, rr[k], gg[k], bb[k]);
+            }
+            const unsigned o = (unsigned)(i * g.W + X);
+            if constexpr (FMT == 0) {
+                uint4 px;
+                px.x = Pix<0>::pack(rr[0], gg[0], bb[0]);
+                px.y = Pix<0>::pack(rr[1], gg[1], bb[1]);
+                px.z = Pix<0>::pack(rr[2], gg[2], bb[2]);
+                px.w = Pix<0>::pack(rr[3], gg[3], bb[3]);
+                st_stream<uint4>(outp, o * 4u, px);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) Pix<1>::store(outp, o + k, rr[k], gg[k], bb[k]);
+            }
+        }
+    }
+}
+
 // K4 for odd W and/or H: the quad's edge then sits half a texel off the
 // texel grid (x0 + 0.5), and CropTexture (.cs:386-410) samples the final
 // texture between two texels (four when both are odd) with weights 1/2: output

@@ -17,35 +17,41 @@ import mmtest as T
 pytestmark = pytest.mark.gpu
 
 
+class _env:
+    """Sets (value str) or removes (None) environment variables for a block."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def _run_env(rows, *args, **kw):
-    old = os.environ.get("MM_K34_ROWS")
-    os.environ["MM_K34_ROWS"] = str(rows)
-    try:
+    with _env(MM_K34_ROWS=str(rows)):
         return T.gpu_run(*args, **kw)
-    finally:
-        if old is None:
-            del os.environ["MM_K34_ROWS"]
-        else:
-            os.environ["MM_K34_ROWS"] = old
 
 
-def _kernels_ran(rows, W, H, n=2, batch=None):
+def _kernels_ran(rows, W, H, n=2, batch=None, oneshot=None):
     """Names of the kernels an n-frame stream launches at this strip size
-    (rows None: the library's own choice by batch size)."""
+    (rows None: the library's own choice by batch size; oneshot "0": short
+    launches keep the unfused K3 -> K4 pair)."""
     import torch
     import mm355
-    old = os.environ.get("MM_K34_ROWS")
-    if rows is None:
-        os.environ.pop("MM_K34_ROWS", None)
-    else:
-        os.environ["MM_K34_ROWS"] = str(rows)
-    try:
+    with _env(MM_K34_ROWS=None if rows is None else str(rows), MM_K34_ONESHOT=oneshot):
         h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=25.0))
-    finally:
-        if old is None:
-            os.environ.pop("MM_K34_ROWS", None)
-        else:
-            os.environ["MM_K34_ROWS"] = old
     if batch:
         h.set_batch(batch)
     fr = torch.zeros((n, H, W, 4), dtype=torch.uint8, device="cuda")
@@ -65,12 +71,59 @@ def test_fused_path_is_selected():
     assert "k_rows_inv_compose" not in _kernels_ran(64, 64, 48)
 
 
+def _fused(ran):
+    return "k_rows_inv_compose" in ran and "k_rows_inv" not in ran and "k_compose" not in ran
+
+
+def _unfused(ran):
+    return "k_rows_inv_compose" not in ran and "k_rows_inv" in ran and "k_compose" in ran
+
+
 def test_strip_policy_by_batch():
-    """Default strip height: fused for many-frame batches, the unfused pair for
-    the one-frame drop-in call (a strip is one sequential workgroup)."""
-    assert "k_rows_inv_compose" not in _kernels_ran(None, 1920, 1080, n=2, batch=1)
-    assert "k_rows_inv_compose" not in _kernels_ran(None, 1920, 1080, n=2, batch=8)
-    assert "k_rows_inv_compose" in _kernels_ran(None, 1920, 1080, n=40, batch=100)
+    """Default policy: the walking strips for many-frame batches; for short
+    launches at N <= 1024 the one-shot form k_rows_inv_compose4 when its 4-row
+    strips fit one workgroup round (960x540 at batch 1: 135 strips), else the
+    unfused pair (always at N = 2048, where the one-shot measured no faster);
+    MM_K34_ONESHOT=0 never, 2 always."""
+    assert _fused(_kernels_ran(None, 960, 540, n=2, batch=1))
+    assert _unfused(_kernels_ran(None, 960, 540, n=2, batch=1, oneshot="0"))
+    assert _unfused(_kernels_ran(None, 1920, 1080, n=2, batch=1))
+    assert _fused(_kernels_ran(None, 1920, 1080, n=2, batch=1, oneshot="2"))
+    assert _unfused(_kernels_ran(None, 1920, 1080, n=2, batch=8))
+    assert _fused(_kernels_ran(None, 1920, 1080, n=40, batch=100))
+
+
+@pytest.mark.parametrize("W,H,edge,fmt,mode", [
+    (200, 120, 0, "f32", "frame"), (200, 118, 1, "u8", "frame"), (240, 136, 1, "u8", "stream"),
+    (504, 250, 0, "u8", "frame"), (120, 200, 1, "f32", "stream"), (1920, 1080, 0, "u8", "frame")])
+def test_oneshot_equals_unfused_bitwise(W, H, edge, fmt, mode):
+    """k_rows_inv_compose4 (forced: MM_K34_ONESHOT=2; one-frame calls and
+    8-frame batches: every strip of 4 output rows in one workgroup of four FFT
+    groups) against the unfused
+    K3 -> K4 pair: the same expressions, so bitwise equal.  H = 118 and 250:
+    a partial last strip; W = 504 at N = 512: the tightest canvas margin."""
+    fr = T.synth(W, H, 4, fmt=fmt)
+    with _env(MM_K34_ROWS=None, MM_K34_ONESHOT="2"):
+        a = T.gpu_run(W, H, fr, 5, 25.0, edge, mode=mode)
+    b = _run_env(0, W, H, fr, 5, 25.0, edge, mode=mode)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_oneshot_standard_mode_and_oracle():
+    W, H = 200, 120
+    fr = T.synth(W, H, 4)
+    std = {"apply": True}
+    with _env(MM_K34_ROWS=None, MM_K34_ONESHOT="2"):
+        a = T.gpu_run(W, H, fr, 5, 25.0, 0, mode="frame", standard=std)
+        got = T.gpu_run(W, H, fr, 5, 25.0, 1, mode="frame")
+    b = _run_env(0, W, H, fr, 5, 25.0, 0, mode="frame", standard=std)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    ref = T.oracle_run(W, H, fr, 5, 25.0, 1)
+    assert np.array_equal(got[0], fr[0])
+    for g, r in zip(got[1:], ref[1:]):
+        T.assert_close_f32(g, r)
 
 
 @pytest.mark.parametrize("W,H,rows,edge,fmt", [
