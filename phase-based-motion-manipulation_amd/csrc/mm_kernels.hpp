@@ -1632,7 +1632,7 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
 // the horizontal 3-tap combine of every staged row and the TR+4 Yh values of the
 // thread's column then live in registers.  One barrier per tile.
 #ifndef MM_K4_ROWS
-#define MM_K4_ROWS 8
+#define MM_K4_ROWS 6   // one-frame calls at 1080p: 8 -> 6 rows per tile 48.4-48.9 -> 47.6-47.8 us per call (4: 49.0-49.2, 16: 49.1-49.8; profiles/r03k_k4_rows_ab.txt)
 #endif
 #ifndef MM_K4_COLS
 #define MM_K4_COLS 256
