@@ -95,7 +95,8 @@ def test_strip_policy_by_batch():
 
 @pytest.mark.parametrize("W,H,edge,fmt,mode", [
     (200, 120, 0, "f32", "frame"), (200, 118, 1, "u8", "frame"), (240, 136, 1, "u8", "stream"),
-    (504, 250, 0, "u8", "frame"), (120, 200, 1, "f32", "stream"), (1920, 1080, 0, "u8", "frame")])
+    (504, 250, 0, "u8", "frame"), (120, 200, 1, "f32", "stream"), (960, 540, 0, "u8", "frame"),
+    (1000, 764, 1, "u8", "stream"), (1920, 1080, 0, "u8", "frame")])
 def test_oneshot_equals_unfused_bitwise(W, H, edge, fmt, mode):
     """k_rows_inv_compose4 (forced: MM_K34_ONESHOT=2; one-frame calls and
     8-frame batches: every strip of 4 output rows in one workgroup of four FFT
