@@ -39,7 +39,9 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 8   /* 8: the state is G_{t-1} (row spectra), see mm_state_size */
+#define MM_ABI_VERSION 9   /* 8: the state is G_{t-1} (row spectra), see mm_state_size;
+                              9: handle-scoped teardown and batch changes (mm_destroy,
+                                 mm_set_batch), no device-wide synchronisation */
 
 /* error codes */
 #define MM_OK               0
@@ -117,7 +119,15 @@ int mm_create(int width, int height, const mm_params *p, int hip_device,
 
 /* OnValidate (.cs:78-88): new parameters apply from the next frame.  Does not
  * synchronise the device: a change of edge_mode (which rewrites the resample
- * tables) waits only for this handle's own latest work. */
+ * tables) waits only for this handle's own latest work.
+ * edge_mode mid-stream: the state is the previous frame's RESAMPLED rows
+ * (G_{t-1}, built with the tables of the call that processed that frame), so
+ * the first frame after an edge_mode change pairs an old-edge G_{t-1} with a
+ * new-edge G_t; from the frame after it both use the new tables.  The
+ * reference re-resamples previousSourceTexture with the current sampler every
+ * frame (.cs:151); its sampler wrap is an unpinned engine choice (SURVEY.md
+ * §8c).  A caller that needs the reference's behaviour exactly calls
+ * mm_reset with the change (that frame then passes through). */
 int mm_set_params(mm_handle *h, const mm_params *p);
 int mm_get_params(const mm_handle *h, mm_params *p);
 
@@ -140,7 +150,9 @@ int mm_process(mm_handle *h, const void *in, void *out, int format, int flags,
 int mm_process_stream(mm_handle *h, const void *in, void *out, int count,
                       int format, void *hip_stream);
 
-/* isFirstFrame = true (.cs:75): the next frame is passed through. */
+/* isFirstFrame = true (.cs:75): the next frame is passed through.  The same
+ * happens after a MM_MODE_STEERABLE mm_set_state followed by a switch to
+ * another mode (that state holds local phases, not G_{t-1}). */
 int mm_reset(mm_handle *h);
 
 /* The temporal state carried between frames (previousSourceTexture, .cs:142):
@@ -169,10 +181,11 @@ void *mm_stream(mm_handle *h);
  * chip across them (each launch first re-transforms the state G_{t-1}).
  * Larger batches amortise that and the launch gaps; the hand-off buffers take
  * about 17.8 MB per 1080p frame (4x at 2160p).  Default: min(64, 2 GiB of
- * buffers).  Results do not depend on the batch size.  Reallocates
- * (synchronises the device); call between frames.  Failure-atomic: on
- * MM_ERR_OOM the handle keeps its previous batch size, buffers and state.
- * Since ABI 5. */
+ * buffers).  Results do not depend on the batch size.  Reallocates: the
+ * old buffers retire behind this handle's latest work and the call waits for
+ * that work only (not for the device, since ABI 9); call between frames.
+ * Failure-atomic: on MM_ERR_OOM the handle keeps its previous batch size,
+ * buffers and state.  Since ABI 5. */
 int mm_set_batch(mm_handle *h, int frames);
 int mm_get_batch(const mm_handle *h, int *frames);
 
@@ -191,7 +204,13 @@ int mm_import_frames(mm_handle *h, int fd, size_t bytes, size_t offset, mm_ext_f
 void *mm_ext_frames_ptr(const mm_ext_frames *x);
 int mm_release_frames(mm_ext_frames *x);
 
-/* OnDestroy/ReleaseResources (.cs:96-99, :344-356). */
+/* OnDestroy/ReleaseResources (.cs:96-99, :344-356).  Returns the handle's
+ * device memory to the device's stream-ordered pool behind the handle's own
+ * latest work (every call that queued work records an event) and waits for
+ * that work only, never for the whole device: other handles and streams on
+ * the GPU keep running.  Work the CALLER queued on its streams that reads
+ * handle-owned memory (none through this API: frames are caller-owned) is the
+ * caller's to finish first.  Since ABI 9. */
 void mm_destroy(mm_handle *h);
 
 const char *mm_strerror(int code);

@@ -66,12 +66,15 @@ struct mm_handle {
     int gs;                     // G slot of the state
     int yh_frames, fb_frames, dbg_frames;  // frames the lazy buffers hold
     hipEvent_t last_ev;         // recorded after this handle's latest work (mm_set_params)
+    hipEvent_t retire_ev;       // orders a buffer's return to the pool behind a call's stream
     bool last_ev_set;
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     bool k2_pow;                // ... and the phase factor as z^S (integer S, MM_K2_PYR_POW)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
+    bool g_valid;               // the G slot gs holds G_{t-1} (K1 or a non-steerable mm_set_state
+                                // wrote it; a steerable mm_set_state sets only the local phases)
     int k2_tail_pct;            // share of a batch's frames of k_cols's packed block run by k_cols_tail
     int k2_tail2_pct;           // share of the second-half blocks' frames run by k_cols's tail blocks
     int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused;
@@ -106,19 +109,39 @@ struct DeviceScope {
     DeviceScope dev_scope_((h)->device);                 \
     if (dev_scope_.err != hipSuccess) return MM_ERR_HIP
 
-// hipMalloc that leaves no error behind on failure: a failed allocation sets
-// the thread's last HIP error, which the next launch check (hipGetLastError)
-// would otherwise report as that launch's failure (an OOM from mm_set_batch
-// must leave the handle usable).
+// Device memory of a handle comes from the device's stream-ordered pool
+// (hipMallocAsync on the handle's own stream) and goes back with hipFreeAsync
+// ordered behind the handle's own work: hipFree would synchronise the whole
+// device (hip_runtime_api.h: "implicit hipDeviceSynchronize"), stalling every
+// other handle and stream on the GPU at a teardown or a batch change
+// (VERDICT r3 #6).  An allocation is made usable on every stream by waiting
+// for the handle's stream (nothing else is queued there).
+// A failed allocation leaves no error behind: the next launch check
+// (hipGetLastError) would otherwise report it as that launch's failure (an
+// OOM from mm_set_batch must leave the handle usable).
 template <class T>
-static hipError_t dev_alloc(T **p, size_t bytes)
+static hipError_t h_alloc(mm_handle *h, T **p, size_t bytes)
 {
-    const hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void **>(p), bytes, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) {
+        if (*p && e != hipErrorOutOfMemory) (void)hipFreeAsync(*p, h->stream);
         *p = nullptr;
         (void)hipGetLastError();
     }
     return e;
+}
+
+// Returns a buffer to the pool once this handle's work that may read it is
+// done: the handle's last call (last_ev) and, when given, what the current
+// call has queued on its stream s so far.  No host wait.
+static void h_retire(mm_handle *h, void *p, hipStream_t s = nullptr, bool have_s = false)
+{
+    if (!p) return;
+    if (h->last_ev_set) (void)hipStreamWaitEvent(h->stream, h->last_ev, 0);
+    if (have_s && s != h->stream && hipEventRecord(h->retire_ev, s) == hipSuccess)
+        (void)hipStreamWaitEvent(h->stream, h->retire_ev, 0);
+    (void)hipFreeAsync(p, h->stream);
 }
 
 // Marks the end of this handle's latest work on stream s (mm_set_params waits
@@ -442,25 +465,23 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
 }
 
 // Grows a per-batch buffer that only some paths use to `frames` frames of
-// `per_frame` bytes.  Growing waits for the device (in-flight work may still
-// read the old buffer); a failed allocation leaves the old one in place.
-static int ensure_frames(void **buf, int *have, int frames, size_t per_frame)
+// `per_frame` bytes.  The old buffer is retired behind this handle's work
+// (its previous calls and what this call queued on s), not behind the
+// device's; a failed allocation leaves the old one in place.
+static int ensure_frames(mm_handle *h, void **buf, int *have, int frames, size_t per_frame, hipStream_t s)
 {
     if (*buf && *have >= frames) return MM_OK;
     void *p = nullptr;
-    if (dev_alloc(&p, per_frame * (size_t)frames) != hipSuccess) return MM_ERR_OOM;
-    if (*buf) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(*buf);
-    }
+    if (h_alloc(h, &p, per_frame * (size_t)frames) != hipSuccess) return MM_ERR_OOM;
+    h_retire(h, *buf, s, true);
     *buf = p;
     *have = frames;
     return MM_OK;
 }
-static int ensure_yh(mm_handle *h)
+static int ensure_yh(mm_handle *h, hipStream_t s)
 {
-    return ensure_frames(reinterpret_cast<void **>(&h->d_Yh), &h->yh_frames, h->chunk,
-                         sizeof(float) * h->yh_stride);
+    return ensure_frames(h, reinterpret_cast<void **>(&h->d_Yh), &h->yh_frames, h->chunk,
+                         sizeof(float) * h->yh_stride, s);
 }
 
 // G slot of the first frame of an n-frame batch: the batch must not
@@ -471,7 +492,7 @@ static int ensure_yh(mm_handle *h)
 static int place_batch(mm_handle *h, int n, hipStream_t s, int *base)
 {
     *base = 0;
-    if (!h->has_state) return MM_OK;
+    if (!h->g_valid) return MM_OK;   // no state slot to keep
     if (h->gs + 1 + n <= h->chunk + 1) {
         *base = h->gs + 1;
         return MM_OK;
@@ -564,7 +585,7 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
     const int ppf = h->geo.Hq / 2;   // whole Q tiles (k_rows_inv)
     const int total = ppf * nout;
     const int gpw = k3_groups<LOG2N>();
-    int rc = ensure_yh(h);
+    int rc = ensure_yh(h, s);
     if (rc) return rc;
     {
         ProfScope ps(h, s, MM_K_ROWS_INV, nout);
@@ -630,23 +651,24 @@ static size_t steer_state_bytes(const mm_handle *h)
 // Band buffers and the temporal state planes for the current levels and
 // orientations.  Reallocated (state invalid) only when those change, never
 // by mm_set_batch: the per-batch spectra Fb grow separately (ensure_frames).
-static int steer_alloc(mm_handle *h)
+static int steer_alloc(mm_handle *h, hipStream_t s)
 {
     const int nb = steer_bands(h);
     const size_t fstride = (size_t)(h->N / 2 + 1) * h->N;
-    int rc = ensure_frames(reinterpret_cast<void **>(&h->d_Fb), &h->fb_frames, h->chunk, sizeof(c2) * fstride);
+    int rc = ensure_frames(h, reinterpret_cast<void **>(&h->d_Fb), &h->fb_frames, h->chunk,
+                           sizeof(c2) * fstride, s);
     if (rc) return rc;
-    if ((rc = ensure_yh(h))) return rc;
+    if ((rc = ensure_yh(h, s))) return rc;
     if (h->steer_nb == nb && h->steer_planes >= steer_planes(h)) return MM_OK;
-    (void)hipDeviceSynchronize();   // in-flight work may still use the old planes
-    (void)hipFree(h->d_T);
-    (void)hipFree(h->d_sst);
+    // in-flight work of this handle may still use the old planes
+    h_retire(h, h->d_T, s, true);
+    h_retire(h, h->d_sst, s, true);
     h->d_T = nullptr;
     h->d_sst = nullptr;
     h->steer_nb = -1;
     h->steer_valid = false;
-    if (dev_alloc(&h->d_T, sizeof(c2) * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
-        dev_alloc(&h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
+    if (h_alloc(h, &h->d_T, sizeof(c2) * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
+        h_alloc(h, &h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
     h->steer_planes = steer_planes(h);
@@ -665,7 +687,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
 {
     constexpr int N = 1 << LOG2N;
     int rc;
-    if ((rc = steer_alloc(h))) return rc;   // may invalidate the handle's planes
+    if ((rc = steer_alloc(h, s))) return rc;   // may invalidate the handle's planes
     const int seed = sst ? 1 : (h->steer_valid ? 0 : 1);
     if (!sst) sst = h->d_sst;
     const size_t fstride = (size_t)(N / 2 + 1) * N;
@@ -721,8 +743,8 @@ static int run_debug(mm_handle *h, uint8_t *out, int n, int first, int fmt, hipS
     if (n <= first) return MM_OK;
     const size_t tex_stride = (size_t)2 * N * N;
     // lazily (only handles that show a debug view pay for it), sized for the batch
-    int rc = ensure_frames(reinterpret_cast<void **>(&h->d_dbg), &h->dbg_frames, h->chunk,
-                           sizeof(float) * tex_stride);
+    int rc = ensure_frames(h, reinterpret_cast<void **>(&h->d_dbg), &h->dbg_frames, h->chunk,
+                           sizeof(float) * tex_stride, s);
     if (rc) return rc;
     if (!h->d_tw_half) {
         std::vector<c2> twh(N / 2);
@@ -730,8 +752,9 @@ static int run_debug(mm_handle *h, uint8_t *out, int n, int first, int fmt, hipS
             const double a = -2.0 * M_PI * (double)k / (double)(N / 2);
             twh[k] = mk((float)cos(a), (float)sin(a));
         }
-        HIPCHK(dev_alloc(&h->d_tw_half, sizeof(c2) * (N / 2)));
-        HIPCHK(hipMemcpy(h->d_tw_half, twh.data(), sizeof(c2) * (N / 2), hipMemcpyHostToDevice));
+        HIPCHK(h_alloc(h, &h->d_tw_half, sizeof(c2) * (N / 2)));
+        HIPCHK(hipMemcpyAsync(h->d_tw_half, twh.data(), sizeof(c2) * (N / 2), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
     }
     const int m = n - first;
     constexpr int T = fft_T<LOG2N - 1>();
@@ -759,16 +782,21 @@ static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
                      hipStream_t s)
 {
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
-    const int first = h->has_state ? 0 : 1;
+    const bool mag = h->p.apply_magnification != 0;
+    const bool dbg = h->p.show_magnitude || h->p.show_phase;
+    // the steerable path's state is its local-phase planes; every other path
+    // needs G_{t-1} in the G slot (a steerable mm_set_state leaves it unset:
+    // the next pyramid frame then passes through, as after a reset)
+    const bool steer = !dbg && h->p.mode == MM_MODE_STEERABLE;
+    const bool have = h->has_state && (steer || h->g_valid);
+    const int first = have ? 0 : 1;
     int rc, base;
     if (first) HIPCHK(hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s));
     if ((rc = place_batch(h, n, s, &base))) return rc;
     c2 *G = h->d_G + h->g_stride * base;
     // G_{t-1}: the state slot; a stream's first frame primes with itself (its
     // Q is computed and not used: it passes through)
-    const c2 *Gprev = h->has_state ? h->d_G + h->g_stride * h->gs : G;
-    const bool mag = h->p.apply_magnification != 0;
-    const bool dbg = h->p.show_magnitude || h->p.show_phase;
+    const c2 *Gprev = have ? h->d_G + h->g_stride * h->gs : G;
     if (!dbg && h->p.mode != MM_MODE_STEERABLE && !mag) {
         // applyMotionMagnification == false: Blit(source, destination) (.cs:139),
         // but previousSourceTexture still follows the input (.cs:142): K1 of
@@ -779,7 +807,7 @@ static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
                                   hipMemcpyDeviceToDevice, s));
         if ((rc = launch_k1<LOG2N>(h, in + fb * (n - 1), 1, fmt, s, G))) return rc;
         h->gs = base;
-        h->has_state = true;
+        h->has_state = h->g_valid = true;
         return MM_OK;
     }
     if ((rc = launch_k1<LOG2N>(h, in, n, fmt, s, G))) return rc;
@@ -795,7 +823,7 @@ static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     }
     if (rc) return rc;
     h->gs = base + n - 1;   // the state follows the input in every mode (.cs:142)
-    h->has_state = true;
+    h->has_state = h->g_valid = true;
     return MM_OK;
 }
 
@@ -938,24 +966,18 @@ int mm_resample_table(int width, int height, int axis, int edge_mode, int32_t *i
 static void free_handle(mm_handle *h)
 {
     if (!h) return;
-    (void)hipFree(h->d_col);
-    (void)hipFree(h->d_row);
-    (void)hipFree(h->d_col3);
-    (void)hipFree(h->d_row3);
-    (void)hipFree(h->d_tw);
-    (void)hipFree(h->d_ktab);
-    (void)hipFree(h->d_tw_half);
-    (void)hipFree(h->d_dbg);
-    (void)hipFree(h->d_Fb);
-    (void)hipFree(h->d_T);
-    (void)hipFree(h->d_sst);
-    (void)hipFree(h->d_G);
-    (void)hipFree(h->d_Q);
-    (void)hipFree(h->d_Yh);
-    (void)hipFree(h->d_stage_in);
-    (void)hipFree(h->d_stage_out);
+    // every buffer back to the pool behind this handle's last work, then wait
+    // for the handle's own stream only (never for the device: VERDICT r3 #6)
+    if (h->stream) {
+        void *bufs[] = {h->d_col, h->d_row, h->d_col3, h->d_row3, h->d_tw, h->d_ktab, h->d_tw_half,
+                        h->d_dbg, h->d_Fb, h->d_T, h->d_sst, h->d_G, h->d_Q, h->d_Yh, h->d_stage_in,
+                        h->d_stage_out};
+        for (void *b : bufs) h_retire(h, b);
+        (void)hipStreamSynchronize(h->stream);
+    }
     if (h->stream) (void)hipStreamDestroy(h->stream);
     if (h->last_ev) (void)hipEventDestroy(h->last_ev);
+    if (h->retire_ev) (void)hipEventDestroy(h->retire_ev);
     for (auto &r : h->prof_recs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -984,21 +1006,26 @@ static int default_batch(int W, int H, int N)
 static int alloc_batch(mm_handle *h, int frames)
 {
     c2 *G = nullptr, *Q = nullptr;
-    if (dev_alloc(&G, sizeof(c2) * h->g_stride * (size_t)(frames + 1)) != hipSuccess ||
-        dev_alloc(&Q, sizeof(c2) * h->q_stride * (size_t)frames) != hipSuccess) {
-        (void)hipFree(G);
+    if (h_alloc(h, &G, sizeof(c2) * h->g_stride * (size_t)(frames + 1)) != hipSuccess ||
+        h_alloc(h, &Q, sizeof(c2) * h->q_stride * (size_t)frames) != hipSuccess) {
+        h_retire(h, G);
         return MM_ERR_OOM;
     }
-    if (h->d_G && h->has_state) {
-        if (hipMemcpy(G + h->g_stride * frames, h->d_G + h->g_stride * h->gs, sizeof(c2) * h->g_stride,
-                      hipMemcpyDeviceToDevice) != hipSuccess) {
-            (void)hipFree(G);
-            (void)hipFree(Q);
+    if (h->d_G && h->g_valid) {
+        // behind the handle's last work (which may still be writing the slot)
+        if (h->last_ev_set) HIPCHK(hipStreamWaitEvent(h->stream, h->last_ev, 0));
+        if (hipMemcpyAsync(G + h->g_stride * frames, h->d_G + h->g_stride * h->gs, sizeof(c2) * h->g_stride,
+                           hipMemcpyDeviceToDevice, h->stream) != hipSuccess) {
+            h_retire(h, G);
+            h_retire(h, Q);
             return MM_ERR_HIP;
         }
     }
-    (void)hipFree(h->d_G);
-    (void)hipFree(h->d_Q);
+    h_retire(h, h->d_G);
+    h_retire(h, h->d_Q);
+    // the new buffers (and the state copy) complete before any later work of
+    // the handle, on whatever stream: a wait for the handle's own stream
+    HIPCHK(hipStreamSynchronize(h->stream));
     h->d_G = G;
     h->d_Q = Q;
     h->gs = frames;
@@ -1045,10 +1072,11 @@ static int upload_tables(mm_handle *h)
     // (taps on i-2 .. i+1) take the Tap4 paths (k_rows_fwd<GEN>, k_compose_odd)
     if (!h->geo.ox && !h->geo.oy && (!taps_local(col) || !taps_local(row))) return MM_ERR_UNSUPPORTED;
     const std::vector<float4> c3 = merge3(col, h->p.edge_mode), r3 = merge3(row, h->p.edge_mode);
-    HIPCHK(hipMemcpy(h->d_col3, c3.data(), sizeof(float4) * h->W, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(h->d_row3, r3.data(), sizeof(float4) * h->H, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(h->d_col, col.data(), sizeof(Tap4) * h->W, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(h->d_row, row.data(), sizeof(Tap4) * h->H, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(h->d_col3, c3.data(), sizeof(float4) * h->W, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d_row3, r3.data(), sizeof(float4) * h->H, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d_col, col.data(), sizeof(Tap4) * h->W, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d_row, row.data(), sizeof(Tap4) * h->H, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));   // the host vectors go out of scope
     return MM_OK;
 }
 
@@ -1120,16 +1148,17 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->yh_stride = (size_t)g.Hq * g.Wy;   // whole Q tiles of rows: K3 stores row pairs
 
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+        hipEventCreateWithFlags(&h->last_ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&h->retire_ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
         free_handle(h);
         return MM_ERR_HIP;
     }
-    bool ok = dev_alloc(&h->d_col, sizeof(Tap4) * width) == hipSuccess &&
-              dev_alloc(&h->d_row, sizeof(Tap4) * height) == hipSuccess &&
-              dev_alloc(&h->d_col3, sizeof(float4) * width) == hipSuccess &&
-              dev_alloc(&h->d_row3, sizeof(float4) * height) == hipSuccess &&
-              dev_alloc(&h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
-              dev_alloc(&h->d_ktab, sizeof(float2) * (size_t)(N / 2 + 1) * ktab_slots(h->log2n)) == hipSuccess &&
+    bool ok = h_alloc(h, &h->d_col, sizeof(Tap4) * width) == hipSuccess &&
+              h_alloc(h, &h->d_row, sizeof(Tap4) * height) == hipSuccess &&
+              h_alloc(h, &h->d_col3, sizeof(float4) * width) == hipSuccess &&
+              h_alloc(h, &h->d_row3, sizeof(float4) * height) == hipSuccess &&
+              h_alloc(h, &h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
+              h_alloc(h, &h->d_ktab, sizeof(float2) * (size_t)(N / 2 + 1) * ktab_slots(h->log2n)) == hipSuccess &&
               alloc_batch(h, h->chunk) == MM_OK;
     if (!ok) {
         free_handle(h);
@@ -1143,7 +1172,8 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
         tw[k].x = (float)cos(a);
         tw[k].y = (float)sin(a);
     }
-    if (hipMemcpy(h->d_tw, tw.data(), sizeof(c2) * ntw, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpyAsync(h->d_tw, tw.data(), sizeof(c2) * ntw, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess) {
         free_handle(h);
         return MM_ERR_HIP;
     }
@@ -1152,6 +1182,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
         return rc;
     }
     h->has_state = false;
+    h->g_valid = false;
     h->steer_nb = -1;
     h->steer_valid = false;
     h->steer_planes = 0;
@@ -1210,7 +1241,8 @@ int mm_set_batch(mm_handle *h, int frames)
     if (!h || frames < 1 || frames > 4096) return MM_ERR_INVALID;
     if (frames == h->chunk) return MM_OK;
     DEVICE_SCOPE(h);
-    HIPCHK(hipDeviceSynchronize());   // in-flight batches use the buffers
+    // the old buffers go back behind this handle's in-flight work (last_ev),
+    // not the device's
     return alloc_batch(h, frames);
 }
 
@@ -1229,8 +1261,11 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
     if (count == 0) return MM_OK;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
+    // last_ev also after a failed call: kernels it launched before failing may
+    // still read the handle's buffers
     const int rc = do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
-    return rc ? rc : note_work(h, s);
+    const int rn = note_work(h, s);
+    return rc ? rc : rn;
 }
 
 int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, void *hip_stream)
@@ -1241,19 +1276,20 @@ int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, v
     // host frames: stage through device buffers and synchronise
     const size_t fb = (size_t)h->W * h->H * (format ? 16 : 4);
     DEVICE_SCOPE(h);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     if (h->stage_bytes < fb) {
-        (void)hipFree(h->d_stage_in);
-        (void)hipFree(h->d_stage_out);
+        h_retire(h, h->d_stage_in, s, true);
+        h_retire(h, h->d_stage_out, s, true);
         h->d_stage_in = h->d_stage_out = nullptr;
         h->stage_bytes = 0;
-        if (dev_alloc(&h->d_stage_in, fb) != hipSuccess || dev_alloc(&h->d_stage_out, fb) != hipSuccess)
+        if (h_alloc(h, &h->d_stage_in, fb) != hipSuccess || h_alloc(h, &h->d_stage_out, fb) != hipSuccess)
             return MM_ERR_OOM;
         h->stage_bytes = fb;
     }
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     HIPCHK(hipMemcpyAsync(h->d_stage_in, in, fb, hipMemcpyHostToDevice, s));
     int rc = do_stream(h, h->d_stage_in, h->d_stage_out, 1, format, s);
-    if (rc || (rc = note_work(h, s))) return rc;
+    const int rn = note_work(h, s);
+    if (rc || (rc = rn)) return rc;
     HIPCHK(hipMemcpyAsync(out, h->d_stage_out, fb, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return MM_OK;
@@ -1263,6 +1299,7 @@ int mm_reset(mm_handle *h)
 {
     if (!h) return MM_ERR_INVALID;
     h->has_state = false;
+    h->g_valid = false;
     h->steer_valid = false;
     return MM_OK;
 }
@@ -1288,6 +1325,7 @@ int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
         HIPCHK(hipMemcpyAsync(dev_buf, h->d_sst, need, hipMemcpyDeviceToDevice, s));
         return note_work(h, s);
     }
+    if (!h->g_valid) return MM_ERR_NO_STATE;
     HIPCHK(hipMemcpyAsync(dev_buf, h->d_G + h->g_stride * h->gs, need, hipMemcpyDeviceToDevice, s));
     return note_work(h, s);
 }
@@ -1299,7 +1337,7 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
     if (h->p.mode == MM_MODE_STEERABLE) {
-        int rc = steer_alloc(h);
+        int rc = steer_alloc(h, s);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(h->d_sst, dev_buf, need, hipMemcpyDeviceToDevice, s));
         h->steer_valid = true;
@@ -1309,6 +1347,7 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
     h->gs = h->chunk;   // the spare slot: between calls no batch occupies G
     HIPCHK(hipMemcpyAsync(h->d_G + h->g_stride * h->gs, dev_buf, need, hipMemcpyDeviceToDevice, s));
     h->has_state = true;
+    h->g_valid = true;
     return note_work(h, s);
 }
 
@@ -1324,14 +1363,18 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
     if (h->p.mode == MM_MODE_STEERABLE && h->p.temporal_filter == MM_FILTER_IIR)
         return MM_ERR_UNSUPPORTED;
     const int rc = do_compute_state(h, (const uint8_t *)in_dev, format, dev_buf, s);
-    return rc ? rc : note_work(h, s);
+    const int rn = note_work(h, s);
+    return rc ? rc : rn;
 }
 
 void mm_destroy(mm_handle *h)
 {
     if (!h) return;
     DeviceScope dev_scope_(h->device);
-    (void)hipDeviceSynchronize();   // work on caller streams may still use the buffers
+    // the buffers go back to the pool behind this handle's last work (last_ev:
+    // every mm_* call that queued work records it), and mm_destroy waits for
+    // that work only; work the caller queued on other streams that reads
+    // handle-owned memory is the caller's to synchronise (include/mm.h)
     free_handle(h);
 }
 

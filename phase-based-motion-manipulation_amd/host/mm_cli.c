@@ -10,6 +10,7 @@
  *          [-b frames_per_call] [-i in.{rgba,y4m}] [-o out.{rgba,y4m}] [-d device]
  *          [--full-range] [--standard] [--show-magnitude] [--show-phase]
  *          [--checksum] [--ring-world G --ring-rank R --ring-id FILE]
+ *          [--ring-local G]
  *
  * --ring-*: frame-sharded synthetic stream over an RCCL ring (include/mm_ring.h,
  * SURVEY.md §8e), one process per GPU: rank R of G processes chunks of -b
@@ -17,6 +18,12 @@
  * to FILE, the others read it.  --checksum prints "frame <t> <byte sum>" per
  * output frame (global frame index t), so a sharded run can be compared with
  * the single-process stream.
+ *
+ * --ring-local G: the same frame-sharded stream at world G inside ONE process
+ * on one device, one thread (and one mm_handle) per rank, through the ring's
+ * test-only local transport (host/mm_ring_local.h): the product's mm_ring_step
+ * logic at world > 1 on a one-GPU box.  Checksums are printed in global frame
+ * order after every rank has finished.
  *
  * .y4m input: 8-bit 4:2:0 / 4:4:4 / mono YUV4MPEG2, geometry from its header
  * (host/y4m.h, BT.601 limited range unless --full-range); .y4m output is 4:4:4
@@ -29,7 +36,11 @@
 
 #include "mm.h"
 #include "mm_ring.h"
+#include "mm_ring_local.h"
 #include "y4m.h"
+
+#include <pthread.h>
+#include <stdint.h>
 
 #include <time.h>
 #include <unistd.h>
@@ -49,19 +60,43 @@ static int ends_with(const char *s, const char *suf)
     return n >= m && strcmp(s + n - m, suf) == 0;
 }
 
-static void print_checksums(const unsigned char *dev, size_t fb, int n, int t0)
+/* 64-bit FNV-1a over the frame's 8-byte words (any changed byte, and any
+ * moved word, changes it; a byte sum would miss permutations) */
+static uint64_t frame_hash(const unsigned char *p, size_t fb)
 {
-    unsigned char *h = (unsigned char *)malloc(fb * (size_t)n);
-    if (!h || hipMemcpy(h, dev, fb * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) {
-        free(h);
-        return;
+    uint64_t h = 0xcbf29ce484222325ull;
+    size_t i = 0;
+    for (; i + 8 <= fb; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
     }
+    for (; i < fb; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+    return h;
+}
+
+/* hashes of n device frames, one frame copied to the host at a time */
+static int hash_frames(const unsigned char *dev, size_t fb, int n, uint64_t *out)
+{
+    unsigned char *h = (unsigned char *)malloc(fb);
+    if (!h) return 1;
     for (int k = 0; k < n; ++k) {
-        unsigned long long sum = 0;
-        for (size_t i = 0; i < fb; ++i) sum += h[fb * (size_t)k + i];
-        printf("frame %d %llu\n", t0 + k, sum);
+        if (hipMemcpy(h, dev + fb * (size_t)k, fb, hipMemcpyDeviceToHost) != hipSuccess) {
+            free(h);
+            return 1;
+        }
+        out[k] = frame_hash(h, fb);
     }
     free(h);
+    return 0;
+}
+
+static void print_checksums(const unsigned char *dev, size_t fb, int n, int t0)
+{
+    uint64_t *hs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1));
+    if (hs && !hash_frames(dev, fb, n, hs))
+        for (int k = 0; k < n; ++k) printf("frame %d %llu\n", t0 + k, (unsigned long long)hs[k]);
+    free(hs);
 }
 
 /* Ring id out of band: rank 0 writes FILE (atomically), the others wait for it. */
@@ -146,11 +181,116 @@ static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world
     return 0;
 }
 
+/* --ring-local: rank threads of one process on one device (test-only transport) */
+typedef struct {
+    mm_ring_hub *hub;
+    const mm_params *p;
+    int W, H, F, B, dev, world, rank, checksum;
+    uint64_t *hashes;   /* [F], global frame index */
+    int rc;
+    char err[256];
+} local_rank;
+
+static void *local_rank_main(void *arg)
+{
+    local_rank *a = (local_rank *)arg;
+    mm_handle *h = NULL;
+    mm_ring *r = NULL;
+    void *d_in = NULL, *d_out = NULL, *d_next = NULL;
+    const size_t fb = (size_t)a->W * a->H * 4;
+    const int steps = a->F / (a->world * a->B);
+    int rc;
+    a->rc = 1;
+    if (hipSetDevice(a->dev) != hipSuccess) { snprintf(a->err, sizeof a->err, "hipSetDevice"); return NULL; }
+    if ((rc = mm_create(a->W, a->H, a->p, a->dev, &h)) || (rc = mm_set_batch(h, a->B)) ||
+        (rc = mm_ring_create_local(a->hub, a->rank, a->dev, h, a->W, a->H, a->B, MM_RGBA8, &r))) {
+        snprintf(a->err, sizeof a->err, "setup: %s (%s)", mm_strerror(rc), mm_ring_last_error());
+        /* a rank that cannot join would leave the others at the hub's
+         * barrier: report and stop the process */
+        fprintf(stderr, "rank %d: %s\n", a->rank, a->err);
+        exit(1);
+    }
+    if (hipMalloc(&d_in, fb * a->B) != hipSuccess || hipMalloc(&d_out, fb * a->B) != hipSuccess ||
+        hipMalloc(&d_next, fb) != hipSuccess) {
+        fprintf(stderr, "rank %d: hipMalloc failed\n", a->rank);
+        exit(1);
+    }
+    hipStream_t s = (hipStream_t)mm_stream(h);
+    for (int st = 0; st < steps; ++st) {
+        const int t0 = st * a->world * a->B + a->rank * a->B;
+        const int more = st + 1 < steps;
+        if ((rc = mm_synth_frames(d_in, a->W, a->H, t0, a->B, 0x5EED0000ull, 0, s)) ||
+            (more && (rc = mm_synth_frames(d_next, a->W, a->H, t0 + a->world * a->B + a->B - 1, 1,
+                                           0x5EED0000ull, 0, s)))) {
+            fprintf(stderr, "rank %d: mm_synth_frames: %s\n", a->rank, mm_strerror(rc));
+            exit(1);
+        }
+        if ((rc = mm_ring_step(r, st, d_in, d_out, more ? d_next : NULL, s))) {
+            fprintf(stderr, "rank %d: mm_ring_step: %s (%s)\n", a->rank, mm_strerror(rc), mm_ring_last_error());
+            exit(1);
+        }
+        if (a->checksum) {
+            if (hipStreamSynchronize(s) != hipSuccess ||
+                hash_frames((const unsigned char *)d_out, fb, a->B, a->hashes + t0)) {
+                fprintf(stderr, "rank %d: readback failed\n", a->rank);
+                exit(1);
+            }
+        }
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) { fprintf(stderr, "rank %d: stream\n", a->rank); exit(1); }
+    mm_ring_destroy(r);
+    mm_destroy(h);
+    hipFree(d_in);
+    hipFree(d_out);
+    hipFree(d_next);
+    a->rc = 0;
+    return NULL;
+}
+
+static int run_ring_local(const mm_params *p, int W, int H, int F, int B, int dev, int world, int checksum)
+{
+    if (world < 1 || world > 64 || F % (world * B) != 0) {
+        fprintf(stderr, "--ring-local: need 1 <= G <= 64 and frames a multiple of G * batch\n");
+        return 2;
+    }
+    mm_ring_hub *hub = NULL;
+    if (mm_ring_hub_create(world, &hub)) return 1;
+    uint64_t *hashes = (uint64_t *)calloc((size_t)F, sizeof(uint64_t));
+    local_rank *ranks = (local_rank *)calloc((size_t)world, sizeof(local_rank));
+    pthread_t *th = (pthread_t *)calloc((size_t)world, sizeof(pthread_t));
+    if (!hashes || !ranks || !th) return 1;
+    for (int g = 0; g < world; ++g) {
+        local_rank *a = &ranks[g];
+        a->hub = hub;
+        a->p = p;
+        a->W = W; a->H = H; a->F = F; a->B = B; a->dev = dev;
+        a->world = world; a->rank = g; a->checksum = checksum;
+        a->hashes = hashes;
+        if (pthread_create(&th[g], NULL, local_rank_main, a) != 0) {
+            fprintf(stderr, "pthread_create failed\n");
+            exit(1);
+        }
+    }
+    int rc = 0;
+    for (int g = 0; g < world; ++g) {
+        pthread_join(th[g], NULL);
+        rc |= ranks[g].rc;
+    }
+    if (!rc && checksum)
+        for (int t = 0; t < F; ++t) printf("frame %d %llu\n", t, (unsigned long long)hashes[t]);
+    printf("ring-local world %d  steps %d  chunk %d\n", world, F / (world * B), B);
+    mm_ring_hub_destroy(hub);
+    free(hashes);
+    free(ranks);
+    free(th);
+    return rc;
+}
+
 int main(int argc, char **argv)
 {
     int W = 1920, H = 1080, F = 300, L = 5, B = 30, dev = 0;
     int full_range = 0, standard = 0, show_mag = 0, show_phase = 0, checksum = 0;
-    int ring_world = 0, ring_rank = 0;
+    int ring_world = 0, ring_rank = 0, ring_local = 0;
     float S = 25.0f;
     const char *in_path = NULL, *out_path = NULL, *ring_id_path = NULL;
     for (int i = 1; i < argc; ++i) {
@@ -174,6 +314,7 @@ int main(int argc, char **argv)
         else if (!strcmp(a, "--ring-world")) ring_world = atoi(v);
         else if (!strcmp(a, "--ring-rank")) ring_rank = atoi(v);
         else if (!strcmp(a, "--ring-id")) ring_id_path = v;
+        else if (!strcmp(a, "--ring-local")) ring_local = atoi(v);
         else { fprintf(stderr, "unknown option %s\n", a); return 2; }
         ++i;
     }
@@ -198,6 +339,13 @@ int main(int argc, char **argv)
     p.mode = standard ? MM_MODE_STANDARD : MM_MODE_PYRAMID;
     p.show_magnitude = show_mag;
     p.show_phase = show_phase;
+    if (ring_local > 0) {
+        if (fi || fo) {
+            fprintf(stderr, "--ring-local needs a synthetic stream\n");
+            return 2;
+        }
+        return run_ring_local(&p, W, H, F, B, dev, ring_local, checksum);
+    }
     /* mm_create runs on `dev` and gives the caller's current device back:
      * this program's own buffers, events and default stream must be on `dev`
      * too (before its first HIP allocation) */

@@ -8,17 +8,35 @@
  * are processed, so the transfer runs under step s's kernels.
  */
 #include "mm_ring.h"
+#include "mm_ring_local.h"
+
+#include <pthread.h>
 
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+/* Transport seam: how one ring shift moves the state.  The product ring uses
+ * RCCL (ncclSend/ncclRecv on the ring's stream); the test-only local
+ * transport (mm_ring_local.h) moves it between threads of one process that
+ * share one GPU, with device copies and events, so that the multi-rank step
+ * logic below runs at world > 1 on a one-GPU box (RCCL refuses two ranks on
+ * one device).  shift(): enqueue on r->cs the send of st_out[k] to rank+1
+ * and the receive of st_in[k] from rank-1; when r->cs passes the shift, the
+ * receive has landed and the peer is done reading st_out[k]. */
+typedef struct {
+    int (*shift)(mm_ring *r, int k);
+    void (*close)(mm_ring *r);
+} ring_ops;
+
 struct mm_ring {
     int world, rank, device, chunk, format;
     size_t frame_bytes, state_bytes;
     mm_handle *h;
-    ncclComm_t comm;
+    const ring_ops *ops;
+    ncclComm_t comm;              /* RCCL transport */
+    mm_ring_hub *hub;             /* local transport */
     hipStream_t cs;               /* the ring's stream */
     void *st_out[2], *st_in[2];   /* per posted step, slot = step & 1 */
     void *carry;                  /* rank 0: st_in of the previous step */
@@ -67,7 +85,7 @@ static void release(mm_ring *r)
 {
     if (!r) return;
     if (r->cs) (void)hipStreamSynchronize(r->cs);
-    if (r->comm) (void)ncclCommDestroy(r->comm);
+    if (r->ops) r->ops->close(r);
     for (int k = 0; k < 2; ++k) {
         (void)hipFree(r->st_out[k]);
         (void)hipFree(r->st_in[k]);
@@ -79,12 +97,33 @@ static void release(mm_ring *r)
     free(r);
 }
 
-int mm_ring_create(int world, int rank, const unsigned char id[MM_RING_ID_BYTES], int hip_device,
-                   mm_handle *h, int width, int height, int chunk, int format, mm_ring **out)
+/* RCCL transport */
+static int nccl_shift(mm_ring *r, int k)
+{
+    const int nxt = (r->rank + 1) % r->world, prv = (r->rank + r->world - 1) % r->world;
+    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(ncclSend(r->st_out[k], r->state_bytes, ncclUint8, nxt, r->comm, r->cs));
+    NCCL_TRY(ncclRecv(r->st_in[k], r->state_bytes, ncclUint8, prv, r->comm, r->cs));
+    NCCL_TRY(ncclGroupEnd());
+    return MM_OK;
+}
+
+static void nccl_close(mm_ring *r)
+{
+    if (r->comm) (void)ncclCommDestroy(r->comm);
+    r->comm = NULL;
+}
+
+static const ring_ops k_nccl_ops = {nccl_shift, nccl_close};
+
+/* Everything but the transport: validates, allocates the state slots, the
+ * ring stream and its events. */
+static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int width, int height,
+                      int chunk, int format, mm_ring **out)
 {
     if (!out) return MM_ERR_INVALID;
     *out = NULL;
-    if (!id || !h || world < 1 || rank < 0 || rank >= world || chunk < 1 || width < 1 || height < 1 ||
+    if (!h || world < 1 || rank < 0 || rank >= world || chunk < 1 || width < 1 || height < 1 ||
         (format != MM_RGBA8 && format != MM_RGBA32F))
         return MM_ERR_INVALID;
     mm_params p;
@@ -125,6 +164,19 @@ int mm_ring_create(int world, int rank, const unsigned char id[MM_RING_ID_BYTES]
         release(r);
         return MM_ERR_OOM;
     }
+    *out = r;
+    return MM_OK;
+}
+
+int mm_ring_create(int world, int rank, const unsigned char id[MM_RING_ID_BYTES], int hip_device,
+                   mm_handle *h, int width, int height, int chunk, int format, mm_ring **out)
+{
+    if (!out) return MM_ERR_INVALID;
+    *out = NULL;
+    if (!id) return MM_ERR_INVALID;
+    mm_ring *r = NULL;
+    int rc = ring_alloc(world, rank, hip_device, h, width, height, chunk, format, &r);
+    if (rc) return rc;
     ncclUniqueId u;
     memcpy(u.internal, id, MM_RING_ID_BYTES);
     ncclResult_t nr = ncclCommInitRank(&r->comm, world, u, rank);
@@ -133,6 +185,96 @@ int mm_ring_create(int world, int rank, const unsigned char id[MM_RING_ID_BYTES]
         release(r);
         return fail_nccl("ncclCommInitRank", nr);
     }
+    r->ops = &k_nccl_ops;
+    *out = r;
+    return MM_OK;
+}
+
+/* ---- local transport (test only: mm_ring_local.h) -------------------------
+ * World ranks are threads of one process on one device.  Per shift, every
+ * rank publishes st_out[k] and an event recorded on its ring stream behind
+ * it; after a host barrier each rank's ring stream waits for its previous
+ * rank's event and copies that rank's st_out[k] into its own st_in[k], then
+ * records `copied`; after a second barrier each ring stream also waits for
+ * its NEXT rank's `copied` (the receiver has read my st_out[k]: what a
+ * completed ncclSend means for the sender's buffer).  The two barriers order
+ * the host-side publication and every event record against the waits on it;
+ * all ranks call shift() in the same order (mm_ring_step's step order), as
+ * RCCL's send/receive pairs require too. */
+#define MM_RING_LOCAL_MAX 64
+struct mm_ring_hub {
+    int world;
+    pthread_barrier_t bar;
+    const void *src[MM_RING_LOCAL_MAX];
+    hipEvent_t posted[MM_RING_LOCAL_MAX], copied[MM_RING_LOCAL_MAX];
+};
+
+int mm_ring_hub_create(int world, mm_ring_hub **out)
+{
+    if (!out) return MM_ERR_INVALID;
+    *out = NULL;
+    if (world < 1 || world > MM_RING_LOCAL_MAX) return MM_ERR_INVALID;
+    mm_ring_hub *hb = (mm_ring_hub *)calloc(1, sizeof *hb);
+    if (!hb) return MM_ERR_OOM;
+    hb->world = world;
+    if (pthread_barrier_init(&hb->bar, NULL, (unsigned)world) != 0) {
+        free(hb);
+        return MM_ERR_OOM;
+    }
+    *out = hb;
+    return MM_OK;
+}
+
+void mm_ring_hub_destroy(mm_ring_hub *hb)
+{
+    if (!hb) return;
+    pthread_barrier_destroy(&hb->bar);
+    free(hb);
+}
+
+static int local_shift(mm_ring *r, int k)
+{
+    mm_ring_hub *hb = r->hub;
+    const int me = r->rank, nxt = (me + 1) % r->world, prv = (me + r->world - 1) % r->world;
+    hb->src[me] = r->st_out[k];
+    HIP_TRY(hipEventRecord(hb->posted[me], r->cs));   /* behind the wait on ready[k] */
+    pthread_barrier_wait(&hb->bar);
+    HIP_TRY(hipStreamWaitEvent(r->cs, hb->posted[prv], 0));
+    HIP_TRY(hipMemcpyAsync(r->st_in[k], hb->src[prv], r->state_bytes, hipMemcpyDeviceToDevice, r->cs));
+    HIP_TRY(hipEventRecord(hb->copied[me], r->cs));
+    pthread_barrier_wait(&hb->bar);
+    HIP_TRY(hipStreamWaitEvent(r->cs, hb->copied[nxt], 0));
+    return MM_OK;
+}
+
+static void local_close(mm_ring *r)
+{
+    if (!r->hub) return;
+    (void)hipEventDestroy(r->hub->posted[r->rank]);
+    (void)hipEventDestroy(r->hub->copied[r->rank]);
+    r->hub->posted[r->rank] = r->hub->copied[r->rank] = NULL;
+    r->hub = NULL;
+}
+
+static const ring_ops k_local_ops = {local_shift, local_close};
+
+int mm_ring_create_local(mm_ring_hub *hub, int rank, int hip_device, mm_handle *h, int width, int height,
+                         int chunk, int format, mm_ring **out)
+{
+    if (!out) return MM_ERR_INVALID;
+    *out = NULL;
+    if (!hub || rank < 0 || rank >= hub->world) return MM_ERR_INVALID;
+    mm_ring *r = NULL;
+    int rc = ring_alloc(hub->world, rank, hip_device, h, width, height, chunk, format, &r);
+    if (rc) return rc;
+    hipError_t e;
+    if ((e = hipEventCreateWithFlags(&hub->posted[rank], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&hub->copied[rank], hipEventDisableTiming)) != hipSuccess) {
+        release(r);
+        return fail_hip("local ring events", e);
+    }
+    r->hub = hub;
+    r->ops = &k_local_ops;
     *out = r;
     return MM_OK;
 }
@@ -146,11 +288,7 @@ static int exchange_begin(mm_ring *r, int step, const void *last, hipStream_t s)
     if (rc) return rc;
     HIP_TRY(hipEventRecord(r->ready[k], s));
     HIP_TRY(hipStreamWaitEvent(r->cs, r->ready[k], 0));
-    const int nxt = (r->rank + 1) % r->world, prv = (r->rank + r->world - 1) % r->world;
-    NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(r->st_out[k], r->state_bytes, ncclUint8, nxt, r->comm, r->cs));
-    NCCL_TRY(ncclRecv(r->st_in[k], r->state_bytes, ncclUint8, prv, r->comm, r->cs));
-    NCCL_TRY(ncclGroupEnd());
+    if ((rc = r->ops->shift(r, k))) return rc;
     HIP_TRY(hipEventRecord(r->done[k], r->cs));
     r->posted[k] = step;
     return MM_OK;

@@ -75,7 +75,7 @@ class Params(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 8   # include/mm.h MM_ABI_VERSION
+ABI_VERSION = 9   # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):

@@ -15,8 +15,8 @@ shift per step carrying the chunk-boundary state to the next rank:
     4. process my C frames.
 
 Overlap (``prefetch=True`` in ``step``): steps 1-2 of step s+1 are posted
-before step s's frames are processed, so the ring transfer (16.8 MB at 1080p,
-about a third of a 30-frame step's compute if it were serialised) runs on
+before step s's frames are processed, so the ring transfer (the state
+G_{t-1}, 8.86 MB at 1080p since ABI 8; ~0.06 ms over one xGMI link) runs on
 the collective's stream underneath step s's kernels; step s+1 then only
 waits for a transfer that has long finished.  This needs step s+1's last
 input frame one step early (one chunk of lookahead); ``finish()`` retires a

@@ -4,32 +4,38 @@
  *   [RequireComponent(typeof(Camera))] MotionMagnificationProcessor.OnRenderImage
  *   (Assets/Scripts/MotionMagnificationProcessor.cs:4-5, :101-143).
  *
- * NOT COMPILED IN THIS REPOSITORY: it needs Unity's PluginAPI headers
- * (IUnityInterface.h, IUnityGraphics.h, IUnityGraphicsVulkan.h, shipped with the
- * editor under Editor/Data/PluginAPI) and the Vulkan SDK headers, neither of
- * which is in this image.  Build it next to a Unity project with
+ * UNVERIFIED SKETCH — NOT COMPILED OR RUN IN THIS REPOSITORY: it needs Unity's
+ * PluginAPI headers (IUnityInterface.h, IUnityGraphics.h, IUnityGraphicsVulkan.h,
+ * shipped with the editor under Editor/Data/PluginAPI) and the Vulkan SDK
+ * headers, neither of which is in this image, and a Unity player to run in.
+ * Build it next to a Unity project with
  *   cc -O2 -fPIC -shared -I<Unity>/Editor/Data/PluginAPI -I<VulkanSDK>/include \
- *      -Iinclude mm_unity_plugin.c -Llib -lmm355 -o Assets/Plugins/x86_64/libmm355_unity.so
+ *      -Iinclude mm_unity_plugin.c -Llib -lmm355 -lvulkan -o Assets/Plugins/x86_64/libmm355_unity.so
  * What it calls on the HIP side (mm_import_frames, mm_process with
  * MM_FRAMES_ON_DEVICE) is built and tested here (tests/test_extmem.py).
  *
- * Data path per frame (render thread, Vulkan renderer):
- *   1. C# OnRenderImage(source, destination) records
- *        cmd.IssuePluginEventAndData(mm_unity_event_func(), MM_UNITY_EVENT_PROCESS, frame)
- *      with `frame` -> struct mm_unity_frame {handle, source, destination textures}.
- *   2. Here, inside Unity's command recording (IUnityGraphicsVulkan::
- *      CommandRecordingState): copy `source` into an exportable linear buffer
- *      (vkCmdCopyImageToBuffer; the RenderTexture's own memory is not
- *      allocated exportable), signal an exportable timeline semaphore.
- *   3. HIP side: the buffers were exported once (vkGetMemoryFdKHR) and imported
- *      once (mm_import_frames); the semaphore likewise (hipImportExternalSemaphore).
- *      hipWaitExternalSemaphoresAsync -> mm_process(in, out, MM_RGBA8,
- *      MM_FRAMES_ON_DEVICE, stream) -> hipSignalExternalSemaphoresAsync.
- *   4. Next recording: wait on that semaphore value and copy the output buffer
- *      into `destination` (vkCmdCopyBufferToImage).
- * The first frame after Start passes through bitwise (.cs:111-117) inside
- * mm_process itself; errors fall back to Graphics.Blit on the C# side
- * (.cs:103-107) because every mm_* call returns a code.
+ * Per frame, ONE render-thread event (C# OnRenderImage(source, destination)
+ * issues cmd.IssuePluginEventAndData(mm_unity_event_func(),
+ * MM_UNITY_EVENT_PROCESS, frame)), configured at load so that Unity submits
+ * the command buffers it has recorded so far (source is rendered) and lets
+ * the plugin submit on the graphics queue itself (ConfigureEvent:
+ * FlushCommandBuffers, queue access Allow, outside a render pass).  One
+ * timeline semaphore shared with HIP orders the three legs of frame i:
+ *
+ *   X_i  (plugin Vulkan submit)  waits 3i   : copy source -> buf[0]     signals 3i+1
+ *   H_i  (HIP, the handle's stream) waits 3i+1: mm_process(buf[0] -> buf[1]) signals 3i+2
+ *   Y_i  (plugin Vulkan submit)  waits 3i+2 : copy buf[1] -> destination signals 3i+3
+ *
+ * so X_{i+1} starts only after Y_i has read buf[1] and H_i has read buf[0],
+ * and destination receives frame i's OWN output within frame i's event (no
+ * one-frame lag).  Frame 0 passes through bitwise inside mm_process
+ * (.cs:111-117), so destination = source on the first frame too.  If
+ * mm_process fails, H_i copies buf[0] to buf[1] instead (the passthrough
+ * Blit of .cs:103-107) and the chain still advances.
+ * The texture layouts are read with AccessTexture(..., ObserveOnly), moved to
+ * TRANSFER_SRC/DST for the copies and restored, inside the plugin's own
+ * command buffers (two sets, re-recorded after a host wait for the value the
+ * set's previous use signalled).
  */
 #include <stdint.h>
 #include <string.h>
@@ -55,13 +61,20 @@ typedef struct mm_unity_frame {
 /* Interop state of one handle: exportable buffers + semaphore, imported once. */
 typedef struct interop {
     mm_handle *h;
+    VkDevice dev;
+    VkQueue queue;
     VkBuffer buf[2];                 /* 0: input frame, 1: output frame (linear RGBA8) */
     VkDeviceMemory mem[2];
     mm_ext_frames *ext[2];           /* the same memory as HIP device pointers */
-    VkSemaphore sem;                 /* timeline: Vulkan copy-in done / HIP done */
+    size_t frame_bytes;
+    VkSemaphore sem;                 /* timeline, values 3i .. 3i+3 for frame i */
     hipExternalSemaphore_t hsem;
-    uint64_t value;
+    uint64_t frame;                  /* frames submitted */
+    VkCommandPool pool;
+    VkCommandBuffer cb[2][2];        /* [set = frame & 1][0: copy in, 1: copy out] */
+    uint64_t set_done[2];            /* timeline value that ends the set's last use */
     hipStream_t stream;
+    PFN_vkWaitSemaphores wait_sem;
 } interop;
 
 static IUnityInterfaces *s_unity;
@@ -90,14 +103,13 @@ static int make_shared_buffer(const UnityVulkanInstance *vi, size_t bytes, int k
     if (vkCreateBuffer(vi->device, &bi, NULL, &s_io.buf[k]) != VK_SUCCESS) return MM_ERR_HIP;
     VkMemoryRequirements req;
     vkGetBufferMemoryRequirements(vi->device, s_io.buf[k], &req);
+    const uint32_t mt = memory_type(vi->physicalDevice, req.memoryTypeBits, VK_MEMORY_PROPERTY_DEVICE_LOCAL_BIT);
+    if (mt == UINT32_MAX) return MM_ERR_UNSUPPORTED;
     VkExportMemoryAllocateInfo ex = {VK_STRUCTURE_TYPE_EXPORT_MEMORY_ALLOCATE_INFO, NULL,
                                      VK_EXTERNAL_MEMORY_HANDLE_TYPE_OPAQUE_FD_BIT};
-    VkMemoryAllocateInfo ai = {VK_STRUCTURE_TYPE_MEMORY_ALLOCATE_INFO, &ex, req.size,
-                               memory_type(vi->physicalDevice, req.memoryTypeBits,
-                                           VK_MEMORY_PROPERTY_DEVICE_LOCAL_BIT)};
-    if (vkAllocateMemory(vi->device, &ai, NULL, &s_io.mem[k]) != VK_SUCCESS ||
-        vkBindBufferMemory(vi->device, s_io.buf[k], s_io.mem[k], 0) != VK_SUCCESS)
-        return MM_ERR_OOM;
+    VkMemoryAllocateInfo ai = {VK_STRUCTURE_TYPE_MEMORY_ALLOCATE_INFO, &ex, req.size, mt};
+    if (vkAllocateMemory(vi->device, &ai, NULL, &s_io.mem[k]) != VK_SUCCESS) return MM_ERR_OOM;
+    if (vkBindBufferMemory(vi->device, s_io.buf[k], s_io.mem[k], 0) != VK_SUCCESS) return MM_ERR_HIP;
     VkMemoryGetFdInfoKHR gi = {VK_STRUCTURE_TYPE_MEMORY_GET_FD_INFO_KHR, NULL, s_io.mem[k],
                                VK_EXTERNAL_MEMORY_HANDLE_TYPE_OPAQUE_FD_BIT};
     int fd = -1;
@@ -106,8 +118,7 @@ static int make_shared_buffer(const UnityVulkanInstance *vi, size_t bytes, int k
     return mm_import_frames(s_io.h, fd, req.size, 0, &s_io.ext[k]);   /* include/mm.h, ABI 6 */
 }
 
-/* Timeline semaphore shared with HIP: Vulkan signals odd values (input copied),
- * HIP signals even values (output written). */
+/* Timeline semaphore (initial value 0) shared with HIP. */
 static int make_shared_semaphore(const UnityVulkanInstance *vi)
 {
     VkSemaphoreTypeCreateInfo ti = {VK_STRUCTURE_TYPE_SEMAPHORE_TYPE_CREATE_INFO, NULL,
@@ -127,69 +138,150 @@ static int make_shared_semaphore(const UnityVulkanInstance *vi)
     hd.type = hipExternalSemaphoreHandleTypeTimelineSemaphoreFd;
     hd.handle.fd = fd;
     if (hipImportExternalSemaphore(&s_io.hsem, &hd) != hipSuccess) return MM_ERR_HIP;
-    return MM_OK;
+    s_io.wait_sem = (PFN_vkWaitSemaphores)vkGetDeviceProcAddr(vi->device, "vkWaitSemaphores");
+    return s_io.wait_sem ? MM_OK : MM_ERR_UNSUPPORTED;
+}
+
+static int make_command_buffers(const UnityVulkanInstance *vi)
+{
+    VkCommandPoolCreateInfo pi = {VK_STRUCTURE_TYPE_COMMAND_POOL_CREATE_INFO, NULL,
+                                  VK_COMMAND_POOL_CREATE_RESET_COMMAND_BUFFER_BIT, vi->queueFamilyIndex};
+    if (vkCreateCommandPool(vi->device, &pi, NULL, &s_io.pool) != VK_SUCCESS) return MM_ERR_HIP;
+    VkCommandBufferAllocateInfo ai = {VK_STRUCTURE_TYPE_COMMAND_BUFFER_ALLOCATE_INFO, NULL, s_io.pool,
+                                      VK_COMMAND_BUFFER_LEVEL_PRIMARY, 4};
+    return vkAllocateCommandBuffers(vi->device, &ai, &s_io.cb[0][0]) == VK_SUCCESS ? MM_OK : MM_ERR_HIP;
 }
 
 /* ---- exported to C# (DllImport "mm355_unity") -------------------------- */
 
+UNITY_INTERFACE_EXPORT void UNITY_INTERFACE_API mm_unity_destroy(mm_handle *h);
+
+/* Start / InitializeProcessor (.cs:90-94).  Vulkan renderer only; on any
+ * failure everything built so far is released and *out is NULL (C# then
+ * keeps the passthrough Blit, .cs:103-107). */
 UNITY_INTERFACE_EXPORT int UNITY_INTERFACE_API mm_unity_create(int width, int height, const mm_params *p,
                                                                mm_handle **out)
 {
-    int rc = mm_create(width, height, p, 0, out);   /* Start / InitializeProcessor (.cs:90-94) */
-    if (rc) return rc;
-    s_io.h = *out;
-    s_io.stream = (hipStream_t)mm_stream(*out);
-    const UnityVulkanInstance vi = s_vulkan->Instance();
-    const size_t bytes = (size_t)width * height * 4;
-    if ((rc = make_shared_buffer(&vi, bytes, 0)) || (rc = make_shared_buffer(&vi, bytes, 1)) ||
-        (rc = make_shared_semaphore(&vi)))
+    if (!out) return MM_ERR_INVALID;
+    *out = NULL;
+    if (!s_vulkan) return MM_ERR_UNSUPPORTED;   /* not the Vulkan renderer (UnityPluginLoad) */
+    if (s_io.h) return MM_ERR_INVALID;          /* one camera per plugin instance */
+    int rc = mm_create(width, height, p, 0, &s_io.h);
+    if (rc) {
+        memset(&s_io, 0, sizeof s_io);
         return rc;
+    }
+    const UnityVulkanInstance vi = s_vulkan->Instance();
+    s_io.dev = vi.device;
+    s_io.queue = vi.graphicsQueue;
+    s_io.stream = (hipStream_t)mm_stream(s_io.h);
+    s_io.frame_bytes = (size_t)width * height * 4;
+    if ((rc = make_shared_buffer(&vi, s_io.frame_bytes, 0)) || (rc = make_shared_buffer(&vi, s_io.frame_bytes, 1)) ||
+        (rc = make_shared_semaphore(&vi)) || (rc = make_command_buffers(&vi))) {
+        mm_unity_destroy(s_io.h);
+        return rc;
+    }
+    *out = s_io.h;
     return MM_OK;
 }
 
-/* Render-thread callback: steps 2-4 of the header comment. */
-static void UNITY_INTERFACE_API on_render_event(int event_id, void *data)
+/* Image barrier inside the plugin's own command buffer. */
+static void transition(VkCommandBuffer cb, VkImage img, VkImageLayout from, VkImageLayout to,
+                       VkAccessFlags src_access, VkAccessFlags dst_access)
 {
-    if (event_id != MM_UNITY_EVENT_PROCESS || !s_vulkan || !data) return;
-    const mm_unity_frame *f = (const mm_unity_frame *)data;
-    UnityVulkanRecordingState rs;
-    if (!s_vulkan->CommandRecordingState(&rs, kUnityVulkanGraphicsQueueAccess_DontCare)) return;
-    VkImageSubresource sub = {VK_IMAGE_ASPECT_COLOR_BIT, 0, 0};
-    UnityVulkanImage src, dst;
-    if (!s_vulkan->AccessTexture(f->source, &sub, VK_IMAGE_LAYOUT_TRANSFER_SRC_OPTIMAL,
-                                 VK_PIPELINE_STAGE_TRANSFER_BIT, VK_ACCESS_TRANSFER_READ_BIT,
-                                 kUnityVulkanResourceAccess_PipelineBarrier, &src) ||
-        !s_vulkan->AccessTexture(f->destination, &sub, VK_IMAGE_LAYOUT_TRANSFER_DST_OPTIMAL,
-                                 VK_PIPELINE_STAGE_TRANSFER_BIT, VK_ACCESS_TRANSFER_WRITE_BIT,
-                                 kUnityVulkanResourceAccess_PipelineBarrier, &dst))
-        return;
+    VkImageMemoryBarrier b;
+    memset(&b, 0, sizeof b);
+    b.sType = VK_STRUCTURE_TYPE_IMAGE_MEMORY_BARRIER;
+    b.srcAccessMask = src_access;
+    b.dstAccessMask = dst_access;
+    b.oldLayout = from;
+    b.newLayout = to;
+    b.srcQueueFamilyIndex = VK_QUEUE_FAMILY_IGNORED;
+    b.dstQueueFamilyIndex = VK_QUEUE_FAMILY_IGNORED;
+    b.image = img;
+    b.subresourceRange.aspectMask = VK_IMAGE_ASPECT_COLOR_BIT;
+    b.subresourceRange.levelCount = 1;
+    b.subresourceRange.layerCount = 1;
+    vkCmdPipelineBarrier(cb, VK_PIPELINE_STAGE_ALL_COMMANDS_BIT, VK_PIPELINE_STAGE_ALL_COMMANDS_BIT, 0, 0, NULL, 0,
+                         NULL, 1, &b);
+}
+
+/* Records the copy between one texture and one interop buffer (to_buffer:
+ * image -> buffer, else buffer -> image), the texture left in its layout. */
+static int record_copy(VkCommandBuffer cb, const UnityVulkanImage *img, VkBuffer buf, int to_buffer,
+                       int width, int height)
+{
+    if (vkResetCommandBuffer(cb, 0) != VK_SUCCESS) return 0;
+    VkCommandBufferBeginInfo bi = {VK_STRUCTURE_TYPE_COMMAND_BUFFER_BEGIN_INFO, NULL,
+                                   VK_COMMAND_BUFFER_USAGE_ONE_TIME_SUBMIT_BIT, NULL};
+    if (vkBeginCommandBuffer(cb, &bi) != VK_SUCCESS) return 0;
+    const VkImageLayout xfer = to_buffer ? VK_IMAGE_LAYOUT_TRANSFER_SRC_OPTIMAL : VK_IMAGE_LAYOUT_TRANSFER_DST_OPTIMAL;
+    const VkAccessFlags acc = to_buffer ? VK_ACCESS_TRANSFER_READ_BIT : VK_ACCESS_TRANSFER_WRITE_BIT;
+    transition(cb, img->image, img->layout, xfer, VK_ACCESS_MEMORY_WRITE_BIT, acc);
     VkBufferImageCopy rg;
     memset(&rg, 0, sizeof rg);
     rg.imageSubresource.aspectMask = VK_IMAGE_ASPECT_COLOR_BIT;
     rg.imageSubresource.layerCount = 1;
-    rg.imageExtent.width = (uint32_t)f->width;
-    rg.imageExtent.height = (uint32_t)f->height;
+    rg.imageExtent.width = (uint32_t)width;
+    rg.imageExtent.height = (uint32_t)height;
     rg.imageExtent.depth = 1;
-    /* the previous frame's output (HIP signalled value) lands in destination */
-    if (s_io.value) vkCmdCopyBufferToImage(rs.commandBuffer, s_io.buf[1], dst.image,
-                                           VK_IMAGE_LAYOUT_TRANSFER_DST_OPTIMAL, 1, &rg);
-    vkCmdCopyImageToBuffer(rs.commandBuffer, src.image, VK_IMAGE_LAYOUT_TRANSFER_SRC_OPTIMAL,
-                           s_io.buf[0], 1, &rg);
-    /* Unity submits rs.commandBuffer; its end-of-frame submit signals
-     * s_io.sem = value+1 (registered through IUnityGraphicsVulkan's
-     * ConfigureEvent / the frame's signal semaphore list). */
-    const uint64_t copied = ++s_io.value;
+    if (to_buffer) vkCmdCopyImageToBuffer(cb, img->image, xfer, buf, 1, &rg);
+    else vkCmdCopyBufferToImage(cb, buf, img->image, xfer, 1, &rg);
+    transition(cb, img->image, xfer, img->layout, acc, VK_ACCESS_MEMORY_READ_BIT | VK_ACCESS_MEMORY_WRITE_BIT);
+    return vkEndCommandBuffer(cb) == VK_SUCCESS;
+}
+
+/* One submission of cb that waits for timeline value `wait` and signals `signal`. */
+static int submit(VkCommandBuffer cb, uint64_t wait, uint64_t signal)
+{
+    VkTimelineSemaphoreSubmitInfo ts = {VK_STRUCTURE_TYPE_TIMELINE_SEMAPHORE_SUBMIT_INFO, NULL, 1, &wait, 1, &signal};
+    const VkPipelineStageFlags stage = VK_PIPELINE_STAGE_TRANSFER_BIT;
+    VkSubmitInfo si = {VK_STRUCTURE_TYPE_SUBMIT_INFO, &ts, 1, &s_io.sem, &stage, 1, &cb, 1, &s_io.sem};
+    return vkQueueSubmit(s_io.queue, 1, &si, VK_NULL_HANDLE) == VK_SUCCESS;
+}
+
+/* Render-thread callback: the three legs of the header comment. */
+static void UNITY_INTERFACE_API on_render_event(int event_id, void *data)
+{
+    if (event_id != MM_UNITY_EVENT_PROCESS || !s_vulkan || !data || !s_io.h) return;
+    const mm_unity_frame *f = (const mm_unity_frame *)data;
+    /* current layouts, no barrier from Unity (the plugin's own command
+     * buffers move and restore them) */
+    VkImageSubresource sub = {VK_IMAGE_ASPECT_COLOR_BIT, 0, 0};
+    UnityVulkanImage src, dst;
+    if (!s_vulkan->AccessTexture(f->source, &sub, VK_IMAGE_LAYOUT_UNDEFINED, 0, 0,
+                                 kUnityVulkanResourceAccess_ObserveOnly, &src) ||
+        !s_vulkan->AccessTexture(f->destination, &sub, VK_IMAGE_LAYOUT_UNDEFINED, 0, 0,
+                                 kUnityVulkanResourceAccess_ObserveOnly, &dst))
+        return;
+    const uint64_t i = s_io.frame, base = 3 * i;
+    const int set = (int)(i & 1);
+    /* the set's command buffers were last submitted for frame i-2 */
+    if (s_io.set_done[set]) {
+        VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &s_io.set_done[set]};
+        if (s_io.wait_sem(s_io.dev, &wi, UINT64_MAX) != VK_SUCCESS) return;
+    }
+    if (!record_copy(s_io.cb[set][0], &src, s_io.buf[0], 1, f->width, f->height) ||
+        !record_copy(s_io.cb[set][1], &dst, s_io.buf[1], 0, f->width, f->height))
+        return;
+    /* X_i: source -> buf[0] after Y_{i-1} (value 3i) */
+    if (!submit(s_io.cb[set][0], base, base + 1)) return;
+    s_io.frame = i + 1;   /* from here on the chain must reach 3i+3 */
+    /* H_i: mm_process on the imported buffers, between 3i+1 and 3i+2 */
     hipExternalSemaphoreWaitParams wp;
     memset(&wp, 0, sizeof wp);
-    wp.params.fence.value = copied;
-    if (hipWaitExternalSemaphoresAsync(&s_io.hsem, &wp, 1, s_io.stream) != hipSuccess) return;
-    if (mm_process(f->h, mm_ext_frames_ptr(s_io.ext[0]), mm_ext_frames_ptr(s_io.ext[1]), MM_RGBA8,
-                   MM_FRAMES_ON_DEVICE, s_io.stream) != MM_OK)
-        return;   /* C# sees no new output and keeps blitting (.cs:103-107) */
+    wp.params.fence.value = base + 1;
+    (void)hipWaitExternalSemaphoresAsync(&s_io.hsem, &wp, 1, s_io.stream);
+    void *in = mm_ext_frames_ptr(s_io.ext[0]), *out = mm_ext_frames_ptr(s_io.ext[1]);
+    if (mm_process(f->h, in, out, MM_RGBA8, MM_FRAMES_ON_DEVICE, s_io.stream) != MM_OK)
+        (void)hipMemcpyAsync(out, in, s_io.frame_bytes, hipMemcpyDeviceToDevice, s_io.stream);   /* .cs:105 */
     hipExternalSemaphoreSignalParams sp;
     memset(&sp, 0, sizeof sp);
-    sp.params.fence.value = ++s_io.value;
+    sp.params.fence.value = base + 2;
     (void)hipSignalExternalSemaphoresAsync(&s_io.hsem, &sp, 1, s_io.stream);
+    /* Y_i: buf[1] -> destination after H_i, in this same event */
+    (void)submit(s_io.cb[set][1], base + 2, base + 3);
+    s_io.set_done[set] = base + 3;
 }
 
 UNITY_INTERFACE_EXPORT UnityRenderingEventAndData UNITY_INTERFACE_API mm_unity_event_func(void)
@@ -197,19 +289,28 @@ UNITY_INTERFACE_EXPORT UnityRenderingEventAndData UNITY_INTERFACE_API mm_unity_e
     return on_render_event;
 }
 
+/* OnDestroy -> ReleaseResources (.cs:96-99): waits for the last frame's chain,
+ * then releases in reverse order of creation (safe on a partial create). */
 UNITY_INTERFACE_EXPORT void UNITY_INTERFACE_API mm_unity_destroy(mm_handle *h)
 {
+    if (!h || h != s_io.h) return;
+    if (s_io.frame && s_io.wait_sem) {
+        const uint64_t last = 3 * s_io.frame;
+        VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &last};
+        (void)s_io.wait_sem(s_io.dev, &wi, UINT64_MAX);
+    }
+    if (s_io.stream) (void)hipStreamSynchronize(s_io.stream);
     for (int k = 0; k < 2; ++k)
         if (s_io.ext[k]) mm_release_frames(s_io.ext[k]);
     if (s_io.hsem) (void)hipDestroyExternalSemaphore(s_io.hsem);
-    mm_destroy(h);                                   /* OnDestroy -> ReleaseResources (.cs:96-99) */
-    if (s_vulkan) {
-        const UnityVulkanInstance vi = s_vulkan->Instance();
+    mm_destroy(h);
+    if (s_io.dev) {
+        if (s_io.pool) vkDestroyCommandPool(s_io.dev, s_io.pool, NULL);   /* frees the command buffers */
         for (int k = 0; k < 2; ++k) {
-            vkDestroyBuffer(vi.device, s_io.buf[k], NULL);
-            vkFreeMemory(vi.device, s_io.mem[k], NULL);
+            if (s_io.buf[k]) vkDestroyBuffer(s_io.dev, s_io.buf[k], NULL);
+            if (s_io.mem[k]) vkFreeMemory(s_io.dev, s_io.mem[k], NULL);
         }
-        vkDestroySemaphore(vi.device, s_io.sem, NULL);
+        if (s_io.sem) vkDestroySemaphore(s_io.dev, s_io.sem, NULL);
     }
     memset(&s_io, 0, sizeof s_io);
 }
@@ -221,6 +322,17 @@ UNITY_INTERFACE_EXPORT void UNITY_INTERFACE_API UnityPluginLoad(IUnityInterfaces
     s_unity = unity;
     s_graphics = UNITY_GET_INTERFACE(unity, IUnityGraphics);
     s_vulkan = UNITY_GET_INTERFACE(unity, IUnityGraphicsVulkan);   /* NULL on other renderers */
+    if (s_vulkan) {
+        /* the event submits on the graphics queue itself: Unity first submits
+         * what it has recorded (the rendered source), outside a render pass */
+        UnityVulkanPluginEventConfig cfg;
+        memset(&cfg, 0, sizeof cfg);
+        cfg.renderPassPrecondition = kUnityVulkanRenderPass_EnsureOutside;
+        cfg.graphicsQueueAccess = kUnityVulkanGraphicsQueueAccess_Allow;
+        cfg.flags = kUnityVulkanEventConfigFlag_EnsurePreviousFrameSubmission |
+                    kUnityVulkanEventConfigFlag_FlushCommandBuffers | kUnityVulkanEventConfigFlag_SyncWorkerThreads;
+        s_vulkan->ConfigureEvent(MM_UNITY_EVENT_PROCESS, &cfg);
+    }
 }
 
 UNITY_INTERFACE_EXPORT void UNITY_INTERFACE_API UnityPluginUnload(void)

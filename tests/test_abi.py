@@ -22,7 +22,7 @@ def test_library_loads_and_exports_header_symbols():
     assert not missing, missing
     for s in syms:
         assert hasattr(L, s)
-    assert L.mm_abi_version() == 8
+    assert L.mm_abi_version() == 9
 
 
 def test_strerror_and_defaults():

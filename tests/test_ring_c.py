@@ -3,9 +3,13 @@ one RCCL ncclSend/ncclRecv per step, driven by the C host (mm_cli --ring-*).
 
 CPU: the library loads, links RCCL and exports every symbol mm_ring.h declares.
 GPU: at world 1 the ring shifts the state to and from the same rank through
-RCCL every step; the output must be bitwise the single-process stream (the
-multi-rank RCCL path runs only on an 8-GPU node: a box here has one GPU, and
-RCCL refuses two ranks on one device).
+RCCL every step; the output must be bitwise the single-process stream.  The
+multi-rank step logic (rank 0's carry of the state received one step earlier,
+both state slots reused, the next step's shift posted ahead) runs at world 2,
+3 and 8 through the ring's test-only local transport (host/mm_ring_local.h:
+rank threads of one process on one GPU, device copies instead of RCCL, which
+refuses two ranks on one device) — `mm_cli --ring-local G`.  RCCL itself at
+world > 1 runs only on an 8-GPU node.
 """
 import os
 import re
@@ -97,3 +101,53 @@ def test_bench_c_ring_world1_1080p_equals_single_rank():
                    "--no-cpu-baseline", "--drop-in-frames", "0"])
     assert "C host RCCL ring" in line["config"]["parallelism"], line["config"]
     assert line["value"] > 0
+
+
+def _cli(args, timeout):
+    env = dict(os.environ, NCCL_DEBUG="WARN")
+    r = subprocess.run([CLI] + args, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return r.stdout
+
+
+def test_ring_local_rejects_uneven_stream():
+    """--ring-local needs the stream to be whole steps of G chunks (checked
+    before any device work)."""
+    r = subprocess.run([CLI, "-w", "64", "-h", "48", "-n", "10", "-b", "4", "--ring-local", "2"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "multiple of G * batch" in r.stderr
+
+
+def test_ring_local_symbols_exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert {"mm_ring_hub_create", "mm_ring_hub_destroy", "mm_ring_create_local"} <= exported
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_c_ring_local_1080p_equals_single_stream(world):
+    """mm_ring_step at world 2 and 3 (rank threads on one GPU,
+    local transport), 1920x1080, chunk 8, 3 steps with the next step's shift
+    posted ahead: per-frame hashes of the whole stream == one rank's stream."""
+    n = world * 8 * 3
+    common = ["-w", "1920", "-h", "1080", "-n", str(n), "-b", "8", "-l", "5", "-s", "25", "--checksum"]
+    a = _checksums(_cli(common, 180))
+    b = _checksums(_cli(common + ["--ring-local", str(world)], 240))
+    assert len(a) == n and a == b
+
+
+@pytest.mark.gpu
+def test_c_ring_local_c4_world8_2400_frames():
+    """C4 itself (BASELINE configs[3]): the 2400-frame 1080p stream frame-
+    sharded over 8 ranks in chunks of 300 (rank threads on one GPU, local
+    transport), per-frame hashes == the single-rank 2400-frame stream; then
+    world 8 with 3 steps of 30-frame chunks (rank 0's carry swap twice, both
+    slots reused)."""
+    common = ["-w", "1920", "-h", "1080", "-l", "5", "-s", "25", "--checksum"]
+    a = _checksums(_cli(common + ["-n", "2400", "-b", "300"], 300))
+    b = _checksums(_cli(common + ["-n", "2400", "-b", "300", "--ring-local", "8"], 300))
+    assert len(a) == 2400 and a == b
+    c = _checksums(_cli(common + ["-n", "720", "-b", "30", "--ring-local", "8"], 240))
+    assert c == a[:720]

@@ -1,0 +1,35 @@
+"""Diagnostic: does a gated stream stay gated, and which handle entry points
+return while another stream is held behind the gate (tests/test_handle.py)."""
+import sys, os, time, threading
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "phase-based-motion-manipulation_amd"))
+import torch, mm355
+from test_handle import _Gate
+
+def probe(name, op):
+    sb = torch.cuda.Stream()
+    g = _Gate()
+    x = torch.zeros(1 << 20, device="cuda")
+    g.hold(sb.cuda_stream)
+    with torch.cuda.stream(sb):
+        x.add_(1)
+    time.sleep(0.2)
+    before = sb.query()
+    th = threading.Thread(target=op)
+    t0 = time.perf_counter()
+    th.start(); th.join(5.0)
+    dt = time.perf_counter() - t0
+    alive = th.is_alive()
+    after = sb.query()
+    g.release(); th.join(); torch.cuda.synchronize(); g.free()
+    print(f"{name}: gate_held_before={not before} op_returned={not alive} ({dt*1e3:.1f} ms) still_pending_after={not after}", flush=True)
+
+probe("noop", lambda: None)
+a = mm355.Handle(64, 48, mm355.Params.make(phase_scale=10.0))
+fr = torch.rand(2, 48, 64, 4, device="cuda"); o = torch.empty_like(fr)
+a.process(fr[0], o[0], mm355.RGBA32F); torch.cuda.synchronize()
+probe("set_params_same_edge", lambda: a.set_params(mm355.Params.make(phase_scale=11.0)))
+probe("set_params_edge", lambda: a.set_params(mm355.Params.make(phase_scale=10.0, edge_mode=mm355.EDGE_CLAMP)))
+probe("set_batch", lambda: a.set_batch(7))
+probe("destroy", a.close)
+probe("create", lambda: mm355.Handle(64, 48, mm355.Params.make(phase_scale=10.0)))
