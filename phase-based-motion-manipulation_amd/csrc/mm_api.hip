@@ -45,6 +45,7 @@ struct mm_handle {
     float4 *d_col3, *d_row3;    // the same taps merged onto offsets -1, 0, +1
     c2 *d_tw;
     float2 *d_ktab;             // K2's per-bin tables of every column (k_k2_table)
+    float *d_kmsum;             // ... and the bins' whole mask sums (pyramid tables)
     int ktab_mode;              // table kind d_ktab holds (-1: stale, refilled before the next K2)
     c2 *d_tw_half;              // W_{N/2} table (debug views, lazily)
     float *d_dbg;               // debug view textures [dbg_frames][mag, phase][N][N] (lazily)
@@ -70,6 +71,7 @@ struct mm_handle {
     bool last_ev_set;
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     bool k2_pow;                // ... and the phase factor as z^S (integer S, MM_K2_PYR_POW)
+    bool k2_tab2;               // ... with overlapping middle bands (MM_K2_PYR_TAB2)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
@@ -300,6 +302,20 @@ static bool bands_fit_table(const Spec &sp)
     return true;
 }
 
+// Two middle bands overlap on an interval of positive width (relative 1e-5:
+// bands that only touch at a mask zero, L <= 5 at the default 0.05 / 0.45,
+// can share a bin by a rounding ulp, which the kernel's per-wave check still
+// routes to the generic op): k_cols runs MM_K2_PYR_TAB2.
+static bool bands_overlap(const Spec &sp)
+{
+    for (int a = 1; a < sp.L - 1; ++a)
+        for (int b = a + 1; b < sp.L - 1; ++b) {
+            const float lo = fmaxf(sp.lo[a], sp.lo[b]), hi = fminf(sp.hi[a], sp.hi[b]);
+            if (hi - lo > 1e-5f * hi) return true;   // NaN bands (L = 3) compare false
+        }
+    return false;
+}
+
 // GaussianBlur.shader:47-60 at _BlurSize 0.5 (.cs:427): bilinear taps at
 // +-0.6923 and +-1.6154 texels == a 5-tap FIR.
 static Blur5 build_blur()
@@ -429,16 +445,14 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
         const int n = (cols + 1) * k2_tab_slots<LOG2N>();
         if (tab_mode == MM_MODE_STANDARD)
             hipLaunchKernelGGL((k_k2_table<LOG2N, MM_MODE_STANDARD>), dim3((n + 255) / 256), dim3(256), 0, s,
-                               h->d_ktab, h->spec);
+                               h->d_ktab, h->d_kmsum, h->spec);
         else
             hipLaunchKernelGGL((k_k2_table<LOG2N, MM_K2_PYR_TAB>), dim3((n + 255) / 256), dim3(256), 0, s,
-                               h->d_ktab, h->spec);
+                               h->d_ktab, h->d_kmsum, h->spec);
         HIPCHK(hipGetLastError());
         h->ktab_mode = tab_mode;
     }
     ProfScope ps(h, s, MM_K_COLS, nframes);
-    // per group: FFT exchange buffer + two per-bin tables (k_cols)
-    const size_t lds = k2_lds_bytes<LOG2N>();
     // the packed block's last k frames go to k_cols_tail (k_cols's critical path)
     int k = nframes >= 24 ? nframes * h->k2_tail_pct / 100 : 0;
     k = std::max(0, std::min(k, nframes - 2));
@@ -448,15 +462,18 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
     const int tb = k2t > 0 ? blocks / 2 : 0;
 #define MM_K2_LAUNCH(MODE)                                                                           \
     do {                                                                                             \
+        const size_t lds = k2_lds_bytes<LOG2N, MODE>(); /* exchange buffers + per-bin tables */      \
         hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks + tb), dim3(k2_threads<LOG2N>()), lds, s, G, \
                            h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, h->d_ktab, \
-                           nframes - k, tb, k2t);                                                    \
+                           h->d_kmsum, nframes - k, tb, k2t);                                        \
         if (k)                                                                                       \
             hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G, \
-                               h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab); \
+                               h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab, \
+                               h->d_kmsum);                                                          \
     } while (0)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
     else if (h->k2_tab && h->k2_pow) MM_K2_LAUNCH(MM_K2_PYR_POW);
+    else if (h->k2_tab2) MM_K2_LAUNCH(MM_K2_PYR_TAB2);
     else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB);
     else MM_K2_LAUNCH(MM_MODE_PYRAMID);
 #undef MM_K2_LAUNCH
@@ -969,7 +986,7 @@ static void free_handle(mm_handle *h)
     // every buffer back to the pool behind this handle's last work, then wait
     // for the handle's own stream only (never for the device: VERDICT r3 #6)
     if (h->stream) {
-        void *bufs[] = {h->d_col, h->d_row, h->d_col3, h->d_row3, h->d_tw, h->d_ktab, h->d_tw_half,
+        void *bufs[] = {h->d_col, h->d_row, h->d_col3, h->d_row3, h->d_tw, h->d_ktab, h->d_kmsum, h->d_tw_half,
                         h->d_dbg, h->d_Fb, h->d_T, h->d_sst, h->d_G, h->d_Q, h->d_Yh, h->d_stage_in,
                         h->d_stage_out};
         for (void *b : bufs) h_retire(h, b);
@@ -1135,6 +1152,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
+    h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
     h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
@@ -1159,6 +1177,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
               h_alloc(h, &h->d_row3, sizeof(float4) * height) == hipSuccess &&
               h_alloc(h, &h->d_tw, sizeof(c2) * tw_entries_v(h->log2n)) == hipSuccess &&
               h_alloc(h, &h->d_ktab, sizeof(float2) * (size_t)(N / 2 + 1) * ktab_slots(h->log2n)) == hipSuccess &&
+              h_alloc(h, &h->d_kmsum, sizeof(float) * (size_t)(N / 2 + 1) * ktab_slots(h->log2n)) == hipSuccess &&
               alloc_batch(h, h->chunk) == MM_OK;
     if (!ok) {
         free_handle(h);
@@ -1215,6 +1234,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     build_spec(*p, h->N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
+    h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
     h->ktab_mode = -1;
     if (edge_changed) return upload_tables(h);
     return MM_OK;

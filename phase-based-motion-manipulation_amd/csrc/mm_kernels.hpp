@@ -175,6 +175,11 @@ __device__ __forceinline__ void st_stream(void *base, unsigned byte_off, T v)
     }
 }
 
+// |z| rows of the row IFFTs (K3 four-wide path, K34, K34o) start kZShift
+// floats into their LDS row, so that the blur taps c-2 .. c+5 of an aligned
+// quad c = x0 + 4q (x0 % 4 == 0) are two 16-B aligned ds_read_b128.
+constexpr int kZShift = 2;
+
 // Q hand-off (K2 -> K3): element (row k, bin f) of a frame, stored in tiles of
 // TK rows: [k/TK][f][k%TK], Qs bins per tile row.  A K2 workgroup's columns of
 // one tile are contiguous (GPW*TK*8 bytes: whole 128-B lines at TK = 8), and
@@ -620,7 +625,19 @@ constexpr int MM_K2_PYR_TAB = 2;
 // fewer issue slots (the scalar bit loop and its phi moves break the bins'
 // interleaving; profiles/r03_ab3.txt).
 constexpr int MM_K2_PYR_POW = 3;
-template <int MODE> constexpr bool k2_tabled() { return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_POW; }
+// MM_K2_PYR_TAB2: MM_K2_PYR_TAB for band layouts whose neighbouring middle
+// bands overlap (L = 6 at the default 0.05 / 0.45: the C3 configuration).
+// Waves holding a two-band bin run pyramid_op_2band_x2 (branch-free, the
+// bins' whole mask sums from a second LDS array) instead of the generic
+// one-bin-at-a-time op; the table is MM_K2_PYR_TAB's.  A separate kernel
+// instance, so that the one-band layouts' kernel keeps its registers.
+constexpr int MM_K2_PYR_TAB2 = 4;
+template <int MODE> constexpr bool k2_tabled()
+{
+    return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_POW || MODE == MM_K2_PYR_TAB2;
+}
+template <int MODE> constexpr bool k2_msum() { return MODE == MM_K2_PYR_TAB2; }
+template <int MODE> constexpr bool k2_one_band_op() { return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_TAB2; }
 
 template <int LOG2N, int MODE>
 __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
@@ -659,6 +676,32 @@ __device__ __forceinline__ float2 bin_static(int fx, int fyy, const Spec &sp)
         // -0.0 included); two bands: y = m_b > 0
         return make_float2(ma, mb != 0.0f ? mb : -(ma + mfix));
     }
+}
+
+// The bin's whole mask sum (every level, the K2 tables' second array): the
+// pass weight of the two-band op.  For a one-band bin it is -y of
+// bin_static's entry bit for bit (the same sum, ma + hp + lp).
+template <int LOG2N>
+__device__ __forceinline__ float bin_mask_sum(int fx, int fyy, const Spec &sp)
+{
+    constexpr int N = 1 << LOG2N;
+    const float ux = (float)fx * (1.0f / (float)N);
+    const float uy = (float)fyy * (1.0f / (float)N);
+    const float fr = __builtin_amdgcn_sqrtf(ux * ux + uy * uy);
+    float mfix = fr > sp.maxF ? 1.0f : (fr > sp.hp_lo ? smooth01((fr - sp.hp_lo) * sp.hp_inv) : 0.0f);
+    if (sp.L > 1)
+        mfix += fr < sp.minF ? 1.0f : (fr < sp.lp_hi ? 1.0f - smooth01((fr - sp.minF) * sp.lp_inv) : 0.0f);
+    float ma = 0.0f, mb = 0.0f;
+    for (int i = 1; i < sp.L - 1; ++i) {
+        if (fr >= sp.lo[i] && fr <= sp.hi[i]) {
+            const float m = 0.5f * (1.0f + __cosf(2.0f * kPi * ((fr - sp.lo[i]) * sp.inv_w[i] - 0.5f)));
+            if (m != 0.0f) {
+                if (ma == 0.0f) ma = m;
+                else mb = m;
+            }
+        }
+    }
+    return mb != 0.0f ? (ma + mb) + mfix : ma + mfix;
 }
 
 // atan2 for a nonzero argument (the magnified bins: |u| = |p||c| > 0 there)
@@ -783,6 +826,65 @@ __device__ __forceinline__ void pyramid_op_1band_x2(c2 &v0, c2 &p0, float2 mt0, 
     p1 = c1;
 }
 
+// pyramid_op_1band_x2 for waves that hold a bin with TWO middle bands (the
+// L = 6 layouts: neighbouring raised-cosine bands overlap), branch-free like
+// the one-band op instead of the generic per-bin path: each band is gated on
+// its own (PyramidPhaseDifference.compute:82-86 per level),
+//   w = msum - mmag + mmag e^{i S delta},  mmag = [m_a not gated] m_a + [m_b not gated] m_b,
+// msum = the bin's whole mask sum (table's second array).  A one-band bin
+// (mt.y < 0) has m_b = 0, whose gate always holds: the one-band op's values
+// bit for bit (msum == -mt.y).
+__device__ __forceinline__ void pyramid_op_2band_x2(c2 &v0, c2 &p0, float2 mt0, float ms0, c2 &v1, c2 &p1,
+                                                    float2 mt1, float ms1, const Spec &sp)
+{
+    const c2 c0 = v0, c1 = v1;
+    const float mn0 = fminf(c0.x * c0.x + c0.y * c0.y, p0.x * p0.x + p0.y * p0.y);
+    const float mn1 = fminf(c1.x * c1.x + c1.y * c1.y, p1.x * p1.x + p1.y * p1.y);
+    const float mb0 = fmaxf(mt0.y, 0.0f), mb1 = fmaxf(mt1.y, 0.0f);
+    const float mmag0 = (mt0.x * mt0.x * mn0 < sp.tau2_nn ? 0.0f : mt0.x) + (mb0 * mb0 * mn0 < sp.tau2_nn ? 0.0f : mb0);
+    const float mmag1 = (mt1.x * mt1.x * mn1 < sp.tau2_nn ? 0.0f : mt1.x) + (mb1 * mb1 * mn1 < sp.tau2_nn ? 0.0f : mb1);
+    const float mpass0 = ms0 - mmag0, mpass1 = ms1 - mmag1;
+    const c2 u0 = mul_conj(p0, c0), u1 = mul_conj(p1, c1);
+    const float ax0 = fabsf(u0.x), ay0 = fabsf(u0.y), ax1 = fabsf(u1.x), ay1 = fabsf(u1.y);
+    const bool st0 = ay0 > ax0, st1 = ay1 > ax1;
+    const float a0 = (st0 ? ax0 : ay0) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(ax0, ay0), 1.17549435e-38f));
+    const float a1 = (st1 ? ax1 : ay1) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(ax1, ay1), 1.17549435e-38f));
+    const c2 a = mk(a0, a1), sq = a * a;
+    c2 r = mk(-0.00405455008149147f, -0.00405455008149147f);
+    r = r * sq + mk(0.021862903609871864f, 0.021862903609871864f);
+    r = r * sq - mk(0.055912263691425323f, 0.055912263691425323f);
+    r = r * sq + mk(0.09642193466424942f, 0.09642193466424942f);
+    r = r * sq - mk(0.1390862911939621f, 0.1390862911939621f);
+    r = r * sq + mk(0.19946566224098206f, 0.19946566224098206f);
+    r = r * sq - mk(0.33329859375953674f, 0.33329859375953674f);
+    r = r * sq + mk(0.9999993443489075f, 0.9999993443489075f);
+    const c2 ra = r * a;
+    const c2 rs = mk(1.57079632679489662f, 1.57079632679489662f) - ra;
+    float t0 = st0 ? rs.x : ra.x, t1 = st1 ? rs.y : ra.y;
+    if (u0.x < 0.0f) t0 = 3.14159265358979324f - t0;
+    if (u1.x < 0.0f) t1 = 3.14159265358979324f - t1;
+    const c2 rev = mk(copysignf(t0, u0.y), copysignf(t1, u1.y)) * mk(sp.S_rev, sp.S_rev);
+    const float cw0 = __builtin_amdgcn_cosf(rev.x), sw0 = __builtin_amdgcn_sinf(rev.x);
+    const float cw1 = __builtin_amdgcn_cosf(rev.y), sw1 = __builtin_amdgcn_sinf(rev.y);
+    v0 = mul(c0, mk(mmag0 * cw0 + mpass0, mmag0 * sw0));
+    v1 = mul(c1, mk(mmag1 * cw1 + mpass1, mmag1 * sw1));
+    p0 = c0;
+    p1 = c1;
+}
+
+// the same for one bin (the packed group's one-at-a-time ops)
+__device__ __forceinline__ c2 pyramid_op_2band(c2 c, c2 p, const Spec &sp, float2 mt, float ms)
+{
+    const float mn2 = fminf(c.x * c.x + c.y * c.y, p.x * p.x + p.y * p.y);
+    const float mb = fmaxf(mt.y, 0.0f);
+    const float mmag = (mt.x * mt.x * mn2 < sp.tau2_nn ? 0.0f : mt.x) + (mb * mb * mn2 < sp.tau2_nn ? 0.0f : mb);
+    const float mpass = ms - mmag;
+    const c2 u = mul_conj(p, c);
+    const float rev = fast_atan2(u.y, u.x) * sp.S_rev;
+    const float cw = __builtin_amdgcn_cosf(rev), sw = __builtin_amdgcn_sinf(rev);
+    return mul(c, mk(mmag * cw + mpass, mmag * sw));
+}
+
 // pyramid_op_1band in the power form (MM_K2_PYR_POW) for NB bins at once (their
 // squarings interleave): v[j] <- c w, prev[j] <- c for j = j0 .. j0 + NB - 1,
 // w = mpass + mmag z^S, the same gate and masks as pyramid_op_1band.
@@ -879,6 +981,13 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
 // k_cols runs at least two columns per workgroup, so that a Q row receives one
 // 16-B (or wider) piece per workgroup instead of one 8-B value per column
 template <int LOG2N> constexpr int k2_groups() { return groups_at_least<LOG2N, MM_K2_GROUPS>(); }
+// K2's Q staging buffer (c2 slots written by rows, read back as float4
+// pieces): slot i lives at i ^ (((i >> 4) & 1) << 1), i.e. float4 r at
+// r ^ ((r >> 3) & 1).  The row writes of a 16-lane group (every other float4
+// of a 16-float4 span) then cover all 32 banks once (linear: 2-way), and the
+// ds_read_b128 groups still read 16 distinct 4-bank slots (tools/lds_banks.py).
+__device__ __forceinline__ int k2_stg_swz(int i) { return i ^ (((i >> 4) & 1) << 1); }
+__device__ __forceinline__ int k2_stg_swz4(int r) { return r ^ ((r >> 3) & 1); }
 template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * fft_T<LOG2N>(); }
 // dynamic LDS of k_cols: per group the FFT exchange buffer and its column's
 // per-bin table, plus for column N/2 (packed group only) its table, its
@@ -893,11 +1002,19 @@ template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * ff
 #define MM_K2_TWTAB 0
 #endif
 template <int LOG2N> constexpr bool k2_twtab() { return MM_K2_TWTAB && fft_c_v(LOG2N) > 1; }
-template <int LOG2N> constexpr size_t k2_lds_bytes()
+// bytes of the mask-sum arrays (pyramid tables: GPW + 1 columns' [TS] floats,
+// rounded up to 16 B)
+template <int LOG2N, int MODE> constexpr size_t k2_msum_bytes()
+{
+    return k2_msum<MODE>()
+               ? ((sizeof(float) * (size_t)(k2_groups<LOG2N>() + 1) * k2_tab_slots<LOG2N>()) + 15) / 16 * 16
+               : 0;
+}
+template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes()
 {
     return (size_t)k2_groups<LOG2N>() *
                (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_slots<LOG2N>()) +
-           sizeof(float2) * k2_tab_slots<LOG2N>() + sizeof(c2) * 4 + sizeof(float) * (1 << LOG2N) +
+           sizeof(float2) * k2_tab_slots<LOG2N>() + k2_msum_bytes<LOG2N, MODE>() + sizeof(c2) * 4 +
            (k2_twtab<LOG2N>() ? sizeof(float4) * tw_tab_float4() : 0);
 }
 
@@ -945,10 +1062,11 @@ template <int LOG2N, int MODE, bool BLK0>
 __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q,
                                             size_t q_stride, int nframes, const Geo &g,
                                             const Spec &sp, const c2 *__restrict__ tw,
-                                            const float2 *__restrict__ ktab, int blk, int nb_prio = 0)
+                                            const float2 *__restrict__ ktab, const float *__restrict__ kmsum,
+                                            int blk, int nb_prio = 0)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
-    constexpr int TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
+    constexpr int TS = k2_tab_slots<LOG2N>();
 #ifdef MM_K2_STAMPS
     const unsigned long long st_entry = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -959,11 +1077,14 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     c2 *lds = lds_all + grp * lds_complex<N>();
     float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TS;
     float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TS;
-    // column N/2: F_{t-1} at its real bins 0 and N/2 (thread 0 of the packed
-    // group), and one frame's Q values by list row (staged like the others: no
-    // global round trip and no store the next frame's loads must wait for)
-    c2 *ldsX = reinterpret_cast<c2 *>(tabN + TS);
-    float *stgN = reinterpret_cast<float *>(ldsX + 4);
+    // column N/2: F_{t-1} at its real bins 0 and N/2 and their results (two
+    // threads of the packed group).  Its Q values are staged with column 0's:
+    // the packed group's staging slot of a row holds (Q0, QN) (the inverse of
+    // A0 + i AN; both real), split into the two columns' pieces at the store.
+    // the bins' whole mask sums (tabled pyramid modes; two-band waves read them)
+    float *ms0 = reinterpret_cast<float *>(tabN + TS) + grp * TS;
+    float *msN = reinterpret_cast<float *>(tabN + TS) + GPW * TS;
+    c2 *ldsX = reinterpret_cast<c2 *>(reinterpret_cast<uint8_t *>(tabN + TS) + k2_msum_bytes<LOG2N, MODE>());
     const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
@@ -1011,7 +1132,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #endif
     // twiddle bases of both FFTs, loaded once (issued under the table copy): no loads inside a frame but G's
     constexpr bool TT = k2_twtab<LOG2N>();
-    float4 *ttab = reinterpret_cast<float4 *>(stgN + N);   // inner passes' twiddle powers (TT)
+    float4 *ttab = reinterpret_cast<float4 *>(ldsX + 4);   // inner passes' twiddle powers (TT)
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
@@ -1031,6 +1152,14 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         if (packed) {
             const float2 *srcN = ktab + (size_t)(N / 2) * TS;
             for (int e = t0; e < TS; e += T) tabN[e] = srcN[e];
+        }
+        if constexpr (k2_msum<MODE>()) {
+            const float *m0 = kmsum + (size_t)f * TS;
+            for (int e = t0; e < TS; e += T) ms0[e] = m0[e];
+            if (packed) {
+                const float *mN = kmsum + (size_t)(N / 2) * TS;
+                for (int e = t0; e < TS; e += T) msN[e] = mN[e];
+            }
         }
         __syncthreads();
     }
@@ -1094,7 +1223,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         const bool ok = e < nq && (GPW <= N / 2 || fb + (2 * r) / TK < N / 2);   // tiny N: fewer columns than groups
         so_st[i] = ok ? (unsigned)((kt * g.Qs + fb) * TK + 2 * r) * 8u : 0x80000000u;
     }
-    const float4 *rd_base = reinterpret_cast<const float4 *>(stg) + grp * T + t0 + rd_off;
+    // (k2_stg_swz: float4 r at r ^ ((r >> 3) & 1); + i GPW T keeps bit 3)
+    const float4 *rd_base = reinterpret_cast<const float4 *>(stg) + k2_stg_swz4(grp * T + t0 + rd_off);
 
     // One straight path per iteration: G loads of frame fr, then the Q stores
     // of frame fr-1 from the staging buffer (exactly NST buffer stores per
@@ -1154,22 +1284,21 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #pragma unroll
             for (int i = 0; i < NST; ++i) {
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 d = {__float_as_uint(sv[i].x), __float_as_uint(sv[i].y),
-                                 __float_as_uint(sv[i].z), __float_as_uint(sv[i].w)};
+                u32x4 d = {__float_as_uint(sv[i].x), __float_as_uint(sv[i].y), __float_as_uint(sv[i].z),
+                           __float_as_uint(sv[i].w)};
+                if constexpr (blk0) {
+                    // a piece of the packed group (column 0: group 0 of block 0)
+                    // holds (Q0, QN) per row: column 0 gets the real parts, column
+                    // N/2 (same rows, N/2 bins further in the tile row) the rest
+                    const int e = grp * T + t + i * GPW * T;
+                    if ((2 * (e % BLK)) / TK == 0) {
+                        const u32x4 dn = {d.y, 0u, d.w, 0u};
+                        d.y = 0u;
+                        d.w = 0u;
+                        __builtin_amdgcn_raw_buffer_store_b128(dn, qrs, so[i] + (unsigned)((N / 2) * TK * 8), 0, 0);
+                    }
+                }
                 __builtin_amdgcn_raw_buffer_store_b128(d, qrs, so[i], 0, 0);
-            }
-            // column N/2 of frame fr-1 (block 0 only).  Read after the barrier:
-            // stgN is rewritten only after the packed section's first barrier below.
-            constexpr int NSTN = blk0 ? (N / 2 + GPW * T - 1) / (GPW * T) : 0;
-#pragma unroll
-            for (int i = 0; i < NSTN; ++i) {
-                const int e = grp * T + t + i * GPW * T;
-                const bool ok = staged && e < g.Hq / 2;   // rows 2e, 2e+1 (one tile: TK even)
-                const float2 p = reinterpret_cast<const float2 *>(stgN)[ok ? e + (cstage ? g.rb / 2 : 0) : 0];
-                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 d = {__float_as_uint(p.x), 0u, __float_as_uint(p.y), 0u};
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    d, qrs, ok ? (unsigned)(((2 * e) / TK * g.Qs + N / 2) * TK + (2 * e) % TK) * 8u : 0x80000000u, 0, 0);
             }
         }
         K2_STAMP(1);
@@ -1218,7 +1347,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     pyramid_op_pow<MM_K2_POWG>(v, prev, j, mt, sp);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-            } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
+            } else if (k2_one_band_op<MODE>() && !wave_two_band) {
                 // no bin of this wave has two middle bands: branch-free op, bins
                 // interleaved MM_K2_OPG at a time
                 // bin j: fy = fy0 + j N/8 (fy0 = fft_bin(t, 0)), table entry fy
@@ -1253,6 +1382,25 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     v[j] = a;
                 }
 #endif
+                __builtin_amdgcn_sched_barrier(0);
+            } else if (MODE == MM_K2_PYR_TAB2) {
+                // a bin of this wave has two middle bands (L = 6 layouts): the
+                // branch-free two-band op, same table addressing + mask sums
+                constexpr int C = fft_c_v(LOG2N);
+                const int fy0 = fft_bin<LOG2N>(HOIST ? t0 : t, 0);
+                const int w = fy0 % C;
+                const float2 *tlo = HOIST ? tlo0 : tab0 + k2_tix<LOG2N>(fy0);
+                const float2 *thi = HOIST ? thi0 : tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
+                const float *mlo = ms0 + (tlo - tab0), *mhi = ms0 + (thi - tab0);
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    if (j % MM_K2_OPX2G == 0) __builtin_amdgcn_sched_barrier(0);
+                    const int i0 = j < 4 ? j * (N / 8) / C : (N - j * (N / 8)) / C;
+                    const int i1 = j + 1 < 4 ? (j + 1) * (N / 8) / C : (N - (j + 1) * (N / 8)) / C;
+                    const float2 mt0 = j < 4 ? tlo[i0] : thi[i0], mt1 = j + 1 < 4 ? tlo[i1] : thi[i1];
+                    const float s0 = j < 4 ? mlo[i0] : mhi[i0], s1 = j + 1 < 4 ? mlo[i1] : mhi[i1];
+                    pyramid_op_2band_x2(v[j], prev[j], mt0, s0, v[j + 1], prev[j + 1], mt1, s1, sp);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             } else {
 #pragma unroll
@@ -1296,7 +1444,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                                                                  : tabN[k2_tix<LOG2N>(N - fy)]};
                             pyramid_op_pow<1>(v, prev, j, mt, sp);
                         }
-                    } else if (MODE == MM_K2_PYR_TAB && !wave_two_band) {
+                    } else if (k2_one_band_op<MODE>() && !wave_two_band) {
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
@@ -1304,6 +1452,17 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                             const c2 c = v[j];
                             v[j] = pyramid_op_1band(c, prev[j], sp, pk_col0(j, fy) ? tab0[k2_tix<LOG2N>(fy)]
                                                                                    : tabN[k2_tix<LOG2N>(N - fy)]);
+                            prev[j] = c;
+                        }
+                    } else if (MODE == MM_K2_PYR_TAB2) {   // two-band waves
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            const int fy = fft_bin<LOG2N>(t, j);
+                            const bool c0 = pk_col0(j, fy);
+                            const int ix = k2_tix<LOG2N>(c0 ? fy : N - fy);
+                            const c2 c = v[j];
+                            v[j] = pyramid_op_2band(c, prev[j], sp, c0 ? tab0[ix] : tabN[ix], c0 ? ms0[ix] : msN[ix]);
                             prev[j] = c;
                         }
                     } else {
@@ -1401,38 +1560,21 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             const int s0 = ((t >> 1) * GPW + grp) * TK + (t & 1);   // T even: (t + jT)/2 = t/2 + jT/2
             if (valid) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    stg[s0 + j * (T / 2) * GPW * TK] = packed ? mk(v[j].x, 0.0f) : v[j];
-                    if (packed) stgN[t + j * T] = v[j].y;
-                }
+                for (int j = 0; j < 8; ++j) stg[k2_stg_swz(s0) + j * (T / 2) * GPW * TK] = v[j];   // packed: (Q0, QN)
             }
         } else if (T % TK == 0 && g.rb >= 0 && g.rb + g.Hq <= N) {
             const int k0 = t - g.rb;   // may be negative: floor division below
             const int s0 = ((k0 >> ilog2c(TK)) * GPW) * TK + (k0 & (TK - 1));
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if (valid && (unsigned)(k0 + j * T) < (unsigned)g.Hq) {
-                    if (packed) {   // inverse of A0 + i AN: real parts Q0 + i QN
-                        stg[s0 + j * T * GPW] = mk(v[j].x, 0.0f);
-                        stgN[k0 + j * T] = v[j].y;
-                    } else {
-                        stg[s0 + j * T * GPW + TK * grp] = v[j];
-                    }
-                }
+                if (valid && (unsigned)(k0 + j * T) < (unsigned)g.Hq)
+                    stg[k2_stg_swz(s0 + j * T * GPW + TK * grp)] = v[j];   // packed (grp 0): (Q0, QN)
             }
         } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-                if (valid && k < g.Hq) {
-                    const int s = ((k / TK) * GPW) * TK + (k % TK);
-                    if (packed) {
-                        stg[s] = mk(v[j].x, 0.0f);
-                        stgN[k] = v[j].y;
-                    } else {
-                        stg[s + TK * grp] = v[j];
-                    }
-                }
+                if (valid && k < g.Hq) stg[k2_stg_swz(((k / TK) * GPW) * TK + (k % TK) + TK * grp)] = v[j];
             }
         }
         }   // !pass_frame
@@ -1459,7 +1601,7 @@ template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
             int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, const float2 *__restrict__ ktab,
-            int nframes_blk0, int tail_blocks, int ktail)
+            const float *__restrict__ kmsum, int nframes_blk0, int tail_blocks, int ktail)
 {
     // Blocks nb .. nb + tail_blocks - 1 (tail_blocks <= nb / 2) are tails: the
     // last ktail frames of the columns of second-half block nb/2 + i, which
@@ -1475,13 +1617,13 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
     // are merged in one L2 (split over XCDs they left as partial-line writes)
     const int blk = xcd_remap(p, nb);
     if (blk == 0) {   // the packed block stops nframes_blk0 frames in (k_cols_tail)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, blk, nb);
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, kmsum, blk, nb);
     } else {
         const int f0 = tail ? nframes - ktail : 0;
         const int nf = tail ? ktail : (p >= nb / 2 && p - nb / 2 < tail_blocks ? nframes - ktail : nframes);
         k_cols_body<LOG2N, MODE, false>(G + (size_t)f0 * g_stride, g_stride,
                                         tail ? G + (size_t)(f0 - 1) * g_stride : Gprev,
-                                        Q + (size_t)f0 * q_stride, q_stride, nf, g, sp, tw, ktab, blk, nb);
+                                        Q + (size_t)f0 * q_stride, q_stride, nf, g, sp, tw, ktab, kmsum, blk, nb);
     }
 }
 
@@ -1497,11 +1639,11 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, int f0, Geo g, Spec sp,
-                 const c2 *__restrict__ tw, const float2 *__restrict__ ktab)
+                 const c2 *__restrict__ tw, const float2 *__restrict__ ktab, const float *__restrict__ kmsum)
 {
     const int fr = f0 + (int)blockIdx.x;   // >= 1
     k_cols_body<LOG2N, MODE, true>(G + (size_t)fr * g_stride, g_stride, G + (size_t)(fr - 1) * g_stride,
-                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, 0);
+                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, kmsum, 0);
 }
 
 // K2's per-bin tables of every column in LDS slot order ([N/2+1][k2_tab_slots]):
@@ -1509,7 +1651,7 @@ void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, int f0, G
 // power of two: exact), evaluated once per parameter set on the launch stream
 // (mm_api.hip launch_k2) instead of in every k_cols workgroup's prologue.
 template <int LOG2N, int MODE>
-__global__ __launch_bounds__(256) void k_k2_table(float2 *__restrict__ ktab, Spec sp)
+__global__ __launch_bounds__(256) void k_k2_table(float2 *__restrict__ ktab, float *__restrict__ kmsum, Spec sp)
 {
     constexpr int N = 1 << LOG2N, TE = k2_tab_entries<LOG2N>(), TS = k2_tab_slots<LOG2N>();
     constexpr int C = fft_c_v(LOG2N), QN = k2_tab_q<LOG2N>();
@@ -1518,12 +1660,15 @@ __global__ __launch_bounds__(256) void k_k2_table(float2 *__restrict__ ktab, Spe
     const int f = id / TS, slot = id - f * TS;
     const int e = C == 1 ? slot : (slot % QN) * C + slot / QN;   // k2_tix(e) == slot
     float2 v = make_float2(0.0f, 0.0f);
+    float ms = 0.0f;
     if (e < TE) {
         const float ks = k2_tabled<MODE>() ? sp.inv_nn : 1.0f;
         const float2 b = bin_static<LOG2N, MODE>(f, e, sp);
         v = make_float2(b.x * ks, b.y * ks);
+        if constexpr (k2_tabled<MODE>()) ms = bin_mask_sum<LOG2N>(f, e, sp) * ks;   // (read by MM_K2_PYR_TAB2)
     }
     ktab[id] = v;
+    if constexpr (k2_tabled<MODE>()) kmsum[id] = ms;
 }
 
 // =========================================================================
@@ -1574,7 +1719,10 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
         v[j] = valid ? mk(q.x - q.w, q.y + q.z) : mk(0.0f, 0.0f); // Z = Qa + i Qb
     }
     fft_regs<LOG2N, +1>(v, t, lds, tw);
-    float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows a, b
+    // the four-wide path reads the |z| rows kZShift floats in (taps c-2 .. c+5
+    // as two aligned ds_read_b128, see k_rows_inv_compose)
+    const bool wide = g.x0 >= 4 && g.x0 % 4 == 0 && g.Wy % 4 == 0 && g.x0 + g.Wy + 4 <= N;
+    float *raw = reinterpret_cast<float *>(lds) + (wide ? kZShift : 0);   // [2][N] |z| of rows a, b
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         raw[t + j * T] = fabsf(v[j].x);
@@ -1583,19 +1731,20 @@ void k_rows_inv(const c2 *__restrict__ Q, size_t q_stride, float *__restrict__ Y
     __syncthreads();
     if (!valid) return;
     float *out = Yh + (size_t)frame * yh_stride + (size_t)ka * g.Wy;
-    if (g.x0 >= 4 && g.x0 % 4 == 0 && g.Wy % 4 == 0 && g.x0 + g.Wy + 4 <= N) {
-        // four outputs per thread from three aligned ds_read_b128 (taps c-2..c+5),
-        // one 16-B store; same expression and order as the scalar form below
+    if (wide) {
+        // four outputs per thread, one 16-B store; same expression and order
+        // as the scalar form below
         const int W4 = g.Wy / 4;
+        const float4 *raw4 = reinterpret_cast<const float4 *>(lds);
         for (int e = t; e < 2 * W4; e += T) {
             const int r = e >= W4 ? 1 : 0, X = 4 * (e - r * W4);
-            const float4 *rw = reinterpret_cast<const float4 *>(raw + r * N + g.x0 + X);
-            const float4 A = rw[-1], B = rw[0], C = rw[1];
+            const float4 *rw = raw4 + ((r * N + g.x0 + X) >> 2);
+            const float4 P = rw[0], Z = rw[1];   // z[c-2 .. c+1], z[c+2 .. c+5]
             float4 o;
-            o.x = bw.w0 * B.x + bw.w1 * (A.w + B.y) + bw.w2 * (A.z + B.z);
-            o.y = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
-            o.z = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
-            o.w = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
+            o.x = bw.w0 * P.z + bw.w1 * (P.y + P.w) + bw.w2 * (P.x + Z.x);
+            o.y = bw.w0 * P.w + bw.w1 * (P.z + Z.x) + bw.w2 * (P.y + Z.y);
+            o.z = bw.w0 * Z.x + bw.w1 * (P.w + Z.y) + bw.w2 * (P.z + Z.z);
+            o.w = bw.w0 * Z.y + bw.w1 * (Z.x + Z.z) + bw.w2 * (P.w + Z.w);
             st_stream<float4>(out, (unsigned)((r * g.Wy + X) * 4), o);
         }
         return;
@@ -1839,7 +1988,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         K34_STAMP(0);
         fft_regs<LOG2N, +1>(v, t, lds, tw);
         K34_STAMP(1);
-        float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows ka, ka+1
+        float *raw = reinterpret_cast<float *>(lds) + kZShift;   // [2][N] |z| of rows ka, ka+1
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             raw[t + j * T] = fabsf(v[j].x);
@@ -1847,16 +1996,22 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         }
         __syncthreads();
         K34_STAMP(2);
-        // ---- horizontal blur of the 4 new list rows (k_rows_inv's float4 form) ----
+        // ---- horizontal blur of the 4 new list rows ----
+        // |z| rows sit 2 floats into their LDS rows (zshift), so the taps
+        // c-2 .. c+5 of the quad are TWO 16-B aligned ds_read_b128 (conflict-
+        // free: consecutive 16 B per lane) instead of the compiler's two
+        // ds_read2_b64 of 8-B aligned halves (2-way conflicts on every one,
+        // tools/lds_banks.py "k34"); same expressions and order as k_rows_inv
+        // one base address; the rows are immediate offsets
+        const float4 *b4 = reinterpret_cast<const float4 *>(raw_all) + ((g.x0 + X) >> 2);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float *rw = raw_all + (r >> 1) * GROUP_FLOATS + (r & 1) * N + g.x0 + X;
-            const float4 *r4 = reinterpret_cast<const float4 *>(rw);
-            const float4 A = r4[-1], B = r4[0], C = r4[1];
-            yw[4 + r][0] = bw.w0 * B.x + bw.w1 * (A.w + B.y) + bw.w2 * (A.z + B.z);
-            yw[4 + r][1] = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
-            yw[4 + r][2] = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
-            yw[4 + r][3] = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
+            const float4 *r4 = b4 + ((r >> 1) * GROUP_FLOATS + (r & 1) * N) / 4;
+            const float4 P = r4[0], Z = r4[1];   // z[c-2 .. c+1], z[c+2 .. c+5]
+            yw[4 + r][0] = bw.w0 * P.z + bw.w1 * (P.y + P.w) + bw.w2 * (P.x + Z.x);
+            yw[4 + r][1] = bw.w0 * P.w + bw.w1 * (P.z + Z.x) + bw.w2 * (P.y + Z.y);
+            yw[4 + r][2] = bw.w0 * Z.x + bw.w1 * (P.w + Z.y) + bw.w2 * (P.z + Z.z);
+            yw[4 + r][3] = bw.w0 * Z.y + bw.w1 * (Z.x + Z.z) + bw.w2 * (P.w + Z.w);
         }
         __syncthreads();   // LDS free for the next step's FFT
         K34_STAMP(3);
@@ -1974,7 +2129,7 @@ void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
             v[j] = valid ? mk(qq.x - qq.w, qq.y + qq.z) : mk(0.0f, 0.0f);
         }
         fft_regs<LOG2N, +1>(v, t, lds, tw);
-        float *raw = reinterpret_cast<float *>(lds);   // [2][N] |z| of rows ka, ka+1
+        float *raw = reinterpret_cast<float *>(lds) + kZShift;   // [2][N] |z| of rows ka, ka+1
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             raw[t + j * T] = fabsf(v[j].x);
@@ -2018,14 +2173,14 @@ void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
     float yw[6][4];               // list rows r0 .. r0+5 of the quad, blurred horizontally
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const int r = 2 * hh + k;   // list row i0 + r: group r/2, row r%2
-        const float *rw = raw_all + (r >> 1) * GROUP_FLOATS + (r & 1) * N + g.x0 + X;
-        const float4 *r4 = reinterpret_cast<const float4 *>(rw);
-        const float4 A = r4[-1], B = r4[0], C = r4[1];
-        yw[k][0] = bw.w0 * B.x + bw.w1 * (A.w + B.y) + bw.w2 * (A.z + B.z);
-        yw[k][1] = bw.w0 * B.y + bw.w1 * (B.x + B.z) + bw.w2 * (A.w + B.w);
-        yw[k][2] = bw.w0 * B.z + bw.w1 * (B.y + B.w) + bw.w2 * (B.x + C.x);
-        yw[k][3] = bw.w0 * B.w + bw.w1 * (B.z + C.x) + bw.w2 * (B.y + C.y);
+        const int r = 2 * hh + k;   // list row i0 + r: group r/2, row r%2 (zshift: k_rows_inv_compose)
+        const float4 *r4 = reinterpret_cast<const float4 *>(raw_all) + ((g.x0 + X) >> 2) +
+                           ((r >> 1) * GROUP_FLOATS + (r & 1) * N) / 4;
+        const float4 P = r4[0], Z = r4[1];   // z[c-2 .. c+1], z[c+2 .. c+5]
+        yw[k][0] = bw.w0 * P.z + bw.w1 * (P.y + P.w) + bw.w2 * (P.x + Z.x);
+        yw[k][1] = bw.w0 * P.w + bw.w1 * (P.z + Z.x) + bw.w2 * (P.y + Z.y);
+        yw[k][2] = bw.w0 * Z.x + bw.w1 * (P.w + Z.y) + bw.w2 * (P.z + Z.z);
+        yw[k][3] = bw.w0 * Z.y + bw.w1 * (Z.x + Z.z) + bw.w2 * (P.w + Z.w);
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {

@@ -246,12 +246,14 @@ def _returns_while_other_stream_gated(op, *, b_frames=8):
     try:
         gate.hold(sb.cuda_stream)
         b.process_stream(frames, outb, b_frames, mm355.RGBA8, stream=sb.cuda_stream)
+        held = not sb.query()
         th.start()
         th.join(20.0)
         returned = not th.is_alive()
         b_pending = not sb.query()
     finally:
         gate.release()
+    assert held, "the gate did not hold B's stream (hipStreamWaitValue32)"
     th.join()
     torch.cuda.synchronize()
     gate.free()
@@ -275,7 +277,8 @@ def test_set_params_does_not_stall_other_streams():
     torch.cuda.synchronize()
     returned, pending, ok_b = _returns_while_other_stream_gated(
         lambda: a.set_params(mm355.Params.make(phase_scale=10.0, edge_mode=mm355.EDGE_CLAMP)))
-    assert returned and pending, "mm_set_params waited for another handle's stream"
+    assert returned, "mm_set_params waited for another handle's stream"
+    assert pending, "B's gated work finished before the gate was released"
     assert ok_b
     a.process(dev[1], oa[1], mm355.RGBA32F)
     a.process(dev[2], oa[2], mm355.RGBA32F)
@@ -305,7 +308,8 @@ def test_set_batch_does_not_stall_other_streams():
     out = torch.empty_like(dev)
     a.process_stream(dev[:3], out[:3], 3, mm355.RGBA32F)
     returned, pending, ok_b = _returns_while_other_stream_gated(lambda: a.set_batch(7))
-    assert returned and pending, "mm_set_batch waited for another handle's stream"
+    assert returned, "mm_set_batch waited for another handle's stream"
+    assert pending, "B's gated work finished before the gate was released"
     assert ok_b
     a.process_stream(dev[3:], out[3:], 5, mm355.RGBA32F)
     torch.cuda.synchronize()
@@ -329,7 +333,8 @@ def test_destroy_does_not_stall_other_streams():
     a.process(np.ascontiguousarray(fr[1]), host_out, mm355.RGBA32F, on_device=False)   # staging
     torch.cuda.synchronize()
     returned, pending, ok_b = _returns_while_other_stream_gated(a.close)
-    assert returned and pending, "mm_destroy waited for another handle's stream"
+    assert returned, "mm_destroy waited for another handle's stream"
+    assert pending, "B's gated work finished before the gate was released"
     assert ok_b
 
 

@@ -26,6 +26,10 @@ GROUPS = {
     "read_b128": (R128, 64, 4),
     "write_b128": ([list(range(i, i + 8)) for i in range(0, 64, 8)], 32, 4),
     "read_b32": ([list(range(0, 32)), list(range(32, 64))], 32, 1),
+    # ds_read2_b64 / ds_read2st64_b64: each of the two 8-B accesses in 4 x 16
+    # contiguous lane groups, banks mod 32 (MI355X_MICROARCH.md §LDS); model
+    # one access per call
+    "read2_b64_access": ([list(range(i, i + 16)) for i in range(0, 64, 16)], 32, 2),
     "write_b32": ([list(range(0, 32)), list(range(32, 64))], 32, 1),
 }
 
@@ -112,7 +116,88 @@ def main():
     report("K2 Q staging write (c2), group 0", "write_b64",
            [[2 * ((((64 * w + l + j * T - rb) % N) // TK) * GPW * TK + ((64 * w + l + j * T - rb) % N) % TK)
              for l in lanes] for w in waves for j in range(8)])
+    # round 4: canvas-row staging slot s0 = ((t >> 1) GPW + grp) TK + (t & 1),
+    # swizzled c2 slot i ^ (((i >> 4) & 1) << 1); reads float4 r ^ ((r >> 3) & 1)
+    swz = lambda i: i ^ (((i >> 4) & 1) << 1)
+    swz4 = lambda r: r ^ ((r >> 3) & 1)
+    for g_ in (0, 1):
+        s0 = lambda t: (((t >> 1) * GPW + g_) * TK + (t & 1))
+        report(f"K2 Q staging write linear, group {g_}", "write_b64",
+               [[2 * (s0(64 * w + l) + j * (T // 2) * GPW * TK) for l in lanes] for w in waves for j in range(8)])
+        report(f"K2 Q staging write swizzled, group {g_}", "write_b64",
+               [[2 * (swz(s0(64 * w + l)) + j * (T // 2) * GPW * TK) for l in lanes] for w in waves for j in range(8)])
+    for off in (0, 482):
+        report(f"K2 Q staging read float4 linear (+{off})", "read_b128",
+               [[4 * (64 * w + l + off) for l in lanes] for w in range(GPW * T // 64)])
+        report(f"K2 Q staging read float4 swizzled (+{off})", "read_b128",
+               [[4 * swz4(64 * w + l + off) for l in lanes] for w in range(GPW * T // 64)])
 
 
 if __name__ == "__main__":
     main()
+
+
+# ---- Stockham passes of fft_regs / fft_pass (mm_fft.hpp) -------------------
+def passes(log2n):
+    out, ns = [], 1
+    full = log2n // 3
+    for p in range((log2n + 2) // 3):
+        r = 8 if p < full else (4 if log2n % 3 == 2 else 2)
+        out.append((r, ns))
+        ns *= r
+    return out
+
+
+def xpad(i, log2n, ns):
+    if log2n < 9 or ns == 1:
+        s, a = 3, 1
+    elif ns == 8:
+        s, a = 5, 4
+    else:
+        s, a = 30, 0
+    return i + a * (i >> s)
+
+
+def stockham_report(tag, log2n, T, waves):
+    """every exchange of the transform over T threads (lane l of wave w:
+    t = 64 w + l): writes y[(b/Ns) Ns R + b%Ns + m Ns], reads x[t + j T]"""
+    N = 1 << log2n
+    ps = passes(log2n)
+    for p, (r, ns) in enumerate(ps[:-1]):
+        B = 8 // r
+        wr = []
+        for w in waves:
+            for q in range(B):
+                for m in range(r):
+                    addrs = []
+                    for l in range(64):
+                        t = 64 * w + l
+                        b = t + q * T
+                        idx = (b // ns) * ns * r + b % ns + m * ns
+                        addrs.append(2 * xpad(idx, log2n, ns))
+                    wr.append(addrs)
+        report(f"{tag} pass {p} (R{r} Ns{ns}) write", "write_b64", wr)
+        rd = [[2 * xpad(64 * w + l + j * T, log2n, ns) for l in range(64)] for w in waves for j in range(8)]
+        report(f"{tag} pass {p} (R{r} Ns{ns}) read", "read_b64", rd)
+
+
+def k34_report(N=2048, x0=64):
+    T = N // 8
+    waves = range(T // 64)
+    stockham_report("K34/K3 fft_regs", N.bit_length() - 1, T, waves)
+    # |z| rows: raw[t + jT], raw[N + t + jT] (floats)
+    report("K34 |z| write raw[t + jT]", "write_b32", [[64 * w + l + j * T for l in range(64)] for w in waves for j in range(8)])
+    # horizontal blur, round 3 code: the compiler read taps c-2 .. c+5 (c = x0 +
+    # 4q) as two ds_read2_b64 of 16 B at 8-B aligned c-2 and c+2 (two accesses
+    # each): 2-way conflicts on every access
+    for c0 in (-2, 0, 2, 4):
+        report(f"K34 blur (r3) read2_b64 access at c{c0:+d}", "read2_b64_access",
+               [[x0 + 4 * (64 * w + l) + c0 for l in range(64)] for w in range(2 * T // 64)])
+    # round 4: |z| rows kZShift = 2 floats in, taps c-2 .. c+5 = two aligned ds_read_b128
+    for k in (0, 1):
+        report(f"K34 blur (r4, zshift) read_b128 #{k}", "read_b128",
+               [[x0 + 4 * (64 * w + l) + 4 * k for l in range(64)] for w in range(2 * T // 64)])
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "k34":
+    k34_report(int(sys.argv[1]))
