@@ -70,7 +70,56 @@ def compulsory_bytes(W, H, N, frames, b_in=4, b_out=4):
             "k_rows_inv_compose": frames * (F * Hq * 8 + W * H * (b_in + b_out))}
 
 
-def parse():
+def steer_bytes_per_frame(W, H, N, L, O, iir, minf=0.05, maxf=0.45, b_in=4, b_out=4):
+    """Compulsory bytes per frame of the steerable extension's kernels (f2,
+    csrc/mm_steer.hpp), by profiling id (mm_profile_end): k_rows_fwd (K1: frame
+    in, G out), k_cols (k_cols_fwd: G in, half spectrum Fb out; k_sb_cols: Fb
+    in, the band rows T out for the columns each band is nonzero in), k_rows_inv
+    (k_sb_rows: T in, the local-phase state planes in and out, Yh out),
+    k_compose (Yh and the frame in, the output frame out).  Band b of middle
+    level i is identically zero in column kx when |kx/N| > hi_i (band_col_zero),
+    so only the other columns' rows are moved."""
+    F, Hn = N // 2 + 1, min(H + 4, N)
+    Hq = Hn + (Hn & 1)
+    Wc = W + 4
+    nmid = L - 2 if L >= 3 else 0
+    nb = nmid * (O // 2)
+    cols = []
+    for i in range(1, L - 1):                       # build_spec (mm_api.hip)
+        r = float("nan") if L == 3 else (i - 1) / (L - 3)
+        c = minf * (maxf / minf) ** (1.0 - r)
+        hi = 1.5 * c
+        n = sum(1 for k in range(N) if not (abs((k if k < N // 2 else k - N) / N) > hi))
+        cols.append(n)
+    t_rows = sum(cols[b % nmid] for b in range(nb)) if nmid else 0
+    t_rows += N                                      # the residual band: every column
+    T_bytes = t_rows * Hq * 8
+    planes = 3 if iir else 1
+    state = nb * Hn * Wc * 4 * planes
+    return {"k_rows_fwd": W * H * b_in + F * H * 8,
+            "k_cols": F * H * 8 + F * N * 8 + F * N * 8 + T_bytes,
+            "k_rows_inv": T_bytes + 2 * state + Hn * W * 4,
+            "k_compose": Hn * W * 4 + W * H * (b_in + b_out)}
+
+
+def profile_key(W, H, L, orientations, standard, filt):
+    """The configuration a committed profile (profiles/traffic.json,
+    profiles/valu.json: their "config" entry) was measured on; bench lines
+    quote PMC traffic and VALU figures only for that configuration."""
+    mode = "standard" if standard else (f"steer{orientations}{filt}" if orientations > 1 else "pyramid")
+    return f"{W}x{H}_L{L}_{mode}"
+
+
+def load_profile(name, key):
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        d = json.load(open(path))
+    except Exception:
+        return None
+    return d if d.get("config") == key else None
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -125,7 +174,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-frames", type=int, default=30, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-keep", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def parse_args(argv):
+    return parse(argv)
 
 
 class GpuBackend:
@@ -376,12 +429,15 @@ def drop_in_per_frame(mm355, torch, params, W, H, frames, local, count):
                        "device-scope HIP events around each call on its stream (second pass)"}
 
 
-def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None, ran=None):
+def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None, ran=None, key=None, per_frame_bytes=None):
     """Frame-level HBM roofline: the design's compulsory bytes per output
     frame (compulsory_bytes() of the kernels that ran, at this batch size, per
     frame) x frames/s per GPU vs 8 TB/s; PMC bytes per frame
     (profiles/traffic.json, rocprofv3 FETCH_SIZE/WRITE_SIZE) beside them."""
-    cb = compulsory_bytes(W, H, N, batch)
+    if per_frame_bytes is not None:    # steerable: bytes per frame by kernel
+        cb = {k: v * batch for k, v in per_frame_bytes.items()}
+    else:
+        cb = compulsory_bytes(W, H, N, batch)
     if ran is None:
         ran = [k for k in cb if k != "k_rows_inv_compose"]
     per_frame = sum(cb[k] for k in ran if k in cb) / batch
@@ -391,10 +447,9 @@ def frame_roofline(W, H, N, fps_per_gpu, batch, dom_traffic=None, ran=None):
            "pmc_bytes_per_frame": None, "pmc_ratio": None,
            "note": "compulsory bytes per frame of the kernels that ran (" + "+".join(ran) +
                    "; DESIGN.md §5) x frames/s per GPU"}
-    tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
+    tj = load_profile("traffic.json", key)
+    if tj is not None:
         try:
-            tj = json.load(open(tfile))
             pmc = sum(tj["kernels"][k]["hbm_bytes_per_frame"] for k in ran)
             rec["pmc_bytes_per_frame"] = int(pmc)
             rec["pmc_ratio"] = round(pmc / per_frame, 4)
@@ -537,10 +592,16 @@ def main():
 
     frames_total = a.steps * C * world
     fps = frames_total / elapsed
+    key = profile_key(W, H, a.levels, a.orientations, a.standard, a.temporal_filter)
+    sbytes = (steer_bytes_per_frame(W, H, N, a.levels, a.orientations, a.temporal_filter == "iir")
+              if steer else None)
     kern = {}
     for name, (ms, launches, nfr) in prof.items():
         if launches:
-            ab = compulsory_bytes(W, H, N, nfr // launches).get(name) if not steer else None
+            if steer:   # bytes per frame x frames over the kernel's summed time
+                ab = round(sbytes[name] * nfr / launches) if name in sbytes else None
+            else:
+                ab = compulsory_bytes(W, H, N, nfr // launches).get(name)
             kern[name] = {"ms_total": round(ms, 4), "launches": launches, "frames": nfr,
                           "us_per_frame": round(ms * 1e3 / nfr, 3),
                           "ms_per_launch": round(ms / launches, 5),
@@ -551,19 +612,18 @@ def main():
     dk = kern[dom]
     achieved = dk["achieved_GBps"]
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
+    tj = load_profile("traffic.json", key)
+    if tj is not None:
         try:
-            tj = json.load(open(tfile))
             pmc_frame = tj["kernels"][dom]["hbm_bytes_per_frame"]
             traffic = round(pmc_frame * dk["frames"] / dk["launches"])
         except Exception:
             traffic = None
     valu = None
-    vfile = os.path.join(ROOT, "profiles", "valu.json")
-    if os.path.exists(vfile):
+    vj_all = load_profile("valu.json", key)
+    if vj_all is not None:
         try:
-            vj = json.load(open(vfile))[dom]
+            vj = vj_all[dom]
             valu = {"valu_busy": vj["valu_busy"], "valu_insts_per_launch": vj["valu_insts_per_launch"],
                     "source": "profiles/valu.json: rocprofv3 SQ_INSTS_VALU x 4 cycles (measured "
                               "issue cost of a wave64 VALU instruction, "
@@ -600,10 +660,12 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 5) if achieved else None,
                      "traffic": traffic,
                      "bytes_model": "compulsory bytes of the dominant kernel (DESIGN.md §5); "
-                                    "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch",
+                                    "traffic = rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch "
+                                    "(profiles/traffic.json, quoted only when measured on this "
+                                    "configuration: " + key + ")",
                      "compute": valu},
-        "frame_roofline": (frame_roofline(W, H, N, fps / world, batch, ran=list(kern))
-                           if not steer else None),
+        "frame_roofline": frame_roofline(W, H, N, fps / world, batch, ran=list(kern), key=key,
+                                         per_frame_bytes=sbytes),
         "survey_model": {"bytes_per_frame": B_survey,
                          "equivalent_GBps_per_gpu": round(B_survey * fps / world / 1e9, 1),
                          "note": "SURVEY.md §8(d) B=W*H*(2b_in+b_out)+6*N^2*8 charges dense "

@@ -72,6 +72,7 @@ struct mm_handle {
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     bool k2_pow;                // ... and the phase factor as z^S (integer S, MM_K2_PYR_POW)
     bool k2_tab2;               // ... with overlapping middle bands (MM_K2_PYR_TAB2)
+    bool k2_stg_ded;            // k_cols stages Q in its own LDS area where it fits (MM_K2_STGD=0: off)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
@@ -462,14 +463,16 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
     const int tb = k2t > 0 ? blocks / 2 : 0;
 #define MM_K2_LAUNCH(MODE)                                                                           \
     do {                                                                                             \
-        const size_t lds = k2_lds_bytes<LOG2N, MODE>(); /* exchange buffers + per-bin tables */      \
+        const int sc2 = h->k2_stg_ded ? k2_stg_c2<LOG2N, MODE>(h->geo.Hq) : 0; /* dedicated staging */ \
+        /* (dedicated staging +) exchange buffers + per-bin tables */                               \
+        const size_t lds = k2_lds_bytes<LOG2N, MODE>() + sizeof(c2) * (size_t)sc2;                   \
         hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks + tb), dim3(k2_threads<LOG2N>()), lds, s, G, \
                            h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, h->d_ktab, \
-                           h->d_kmsum, nframes - k, tb, k2t);                                        \
+                           h->d_kmsum, sc2, nframes - k, tb, k2t);                                   \
         if (k)                                                                                       \
             hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G, \
                                h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab, \
-                               h->d_kmsum);                                                          \
+                               h->d_kmsum, sc2);                                                     \
     } while (0)
     if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
     else if (h->k2_tab && h->k2_pow) MM_K2_LAUNCH(MM_K2_PYR_POW);
@@ -1156,6 +1159,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
+    h->k2_stg_ded = !(getenv("MM_K2_STGD") && atoi(getenv("MM_K2_STGD")) == 0);
     h->k2_tail2_pct = getenv("MM_K2_TAIL2") ? atoi(getenv("MM_K2_TAIL2")) : 10;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
     h->k34_oneshot = getenv("MM_K34_ONESHOT") ? atoi(getenv("MM_K34_ONESHOT")) : 1;

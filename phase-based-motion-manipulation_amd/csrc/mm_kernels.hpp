@@ -1002,6 +1002,17 @@ template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * ff
 #define MM_K2_TWTAB 0
 #endif
 template <int LOG2N> constexpr bool k2_twtab() { return MM_K2_TWTAB && fft_c_v(LOG2N) > 1; }
+// Dedicated Q staging (k_cols_body stg_c2): the list rows [0, Hq) of the
+// workgroup's GPW columns, [Hq/TK][GPW][TK] c2 (k2_stg_swz stays inside
+// 32-slot blocks), when it fits beside two workgroups per CU (1080p: 17 KB);
+// else 0 (aliased with the exchange buffers).
+template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes();
+template <int LOG2N, int MODE> inline int k2_stg_c2(int Hq)
+{
+    const int c = (Hq * k2_groups<LOG2N>() + 31) / 32 * 32;
+    return k2_lds_bytes<LOG2N, MODE>() + sizeof(c2) * (size_t)c <= 81920 ? c : 0;
+}
+
 // bytes of the mask-sum arrays (pyramid tables: GPW + 1 columns' [TS] floats,
 // rounded up to 16 B)
 template <int LOG2N, int MODE> constexpr size_t k2_msum_bytes()
@@ -1063,7 +1074,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                                             size_t q_stride, int nframes, const Geo &g,
                                             const Spec &sp, const c2 *__restrict__ tw,
                                             const float2 *__restrict__ ktab, const float *__restrict__ kmsum,
-                                            int blk, int nb_prio = 0)
+                                            int stg_c2, int blk, int nb_prio = 0)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
     constexpr int TS = k2_tab_slots<LOG2N>();
@@ -1074,9 +1085,14 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     // group index: wave-uniform (scalar) when a group spans whole waves
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
     const int t0 = threadIdx.x % T;
-    c2 *lds = lds_all + grp * lds_complex<N>();
-    float2 *tab0 = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + grp * TS;
-    float2 *tabN = reinterpret_cast<float2 *>(lds_all + GPW * lds_complex<N>()) + GPW * TS;
+    // stg_c2 > 0: a dedicated Q staging area of that many c2 at the start of
+    // the LDS (k2_stg_c2, when it fits beside two workgroups per CU), the FFT
+    // exchange buffers and tables after it; 0: the staging aliases the
+    // exchange buffers (two more workgroup barriers per frame)
+    c2 *xbase = lds_all + stg_c2;
+    c2 *lds = xbase + grp * lds_complex<N>();
+    float2 *tab0 = reinterpret_cast<float2 *>(xbase + GPW * lds_complex<N>()) + grp * TS;
+    float2 *tabN = reinterpret_cast<float2 *>(xbase + GPW * lds_complex<N>()) + GPW * TS;
     // column N/2: F_{t-1} at its real bins 0 and N/2 and their results (two
     // threads of the packed group).  Its Q values are staged with column 0's:
     // the packed group's staging slot of a row holds (Q0, QN) (the inverse of
@@ -1204,13 +1220,14 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     constexpr int NST = (N * GPW / 2 + GPW * T - 1) / (GPW * T);   // store slots per thread (Hq <= N)
     const int fb = blk * GPW, nq = (g.Hq / TK) * BLK;
     c2 *stg = lds_all;   // staged Q pieces of a frame: [row pair][GPW][TK]
+    const bool stg_ded = stg_c2 > 0;
     bool staged = false;   // stg holds the previous frame's pieces (uniform)
     // Canvas-row staging (TK == 2, rb even, no list row wrapping: every
     // geometry but H close to N): the inverse transform's rows n = t + jT go
     // to LDS unconditionally at slot(n) = ((n/2) GPW + grp) TK + n%2 (one base
     // + immediates, no per-row checks), and the Q stores read list row pair kt
     // at canvas pair kt + rb/2.  Otherwise list-row staging (rows of [0, Hq)).
-    const bool cstage = TK == 2 && (g.rb & 1) == 0 && g.rb >= 0 && g.rb + g.Hq <= N;
+    const bool cstage = !stg_ded && TK == 2 && (g.rb & 1) == 0 && g.rb >= 0 && g.rb + g.Hq <= N;
     const int rd_off = cstage ? (g.rb / 2) * GPW : 0;   // float4 pieces
     // frame-invariant per-thread Q store offsets (loop invariant: computed
     // from t0, not the opaque t below); a frame with nothing staged stores
@@ -1265,7 +1282,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             float4 sv[NST];
 #pragma unroll
             for (int i = 0; i < NST; ++i) sv[i] = rd_base[i * GPW * T];   // (slots past the staging: unused)
-            __syncthreads();   // staging read before this frame's FFT rewrites the buffers
+            // (aliased staging) staging read before this frame's FFT rewrites the buffers
+            if (!stg_ded) __syncthreads();
             const int qfr = __builtin_amdgcn_readfirstlane(fr > 0 ? fr - 1 : 0);   // uniform
             const auto qrs = __builtin_amdgcn_make_buffer_rsrc(
                 Q + (size_t)qfr * q_stride, 0, staged ? (int)(q_stride * sizeof(c2)) : 0, 0x00020000);
@@ -1546,7 +1564,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         fft_dit<LOG2N, +1, TT>(v, t, lds, wt, ttab);   // natural row order again
         MM_MARK("M4_inv_end");
         K2_STAMP(5);
-        __syncthreads();   // every wave past its exchange reads: the staging overwrites them
+        if (!stg_ded) __syncthreads();   // (aliased) every wave past its exchange reads: the staging overwrites them
         // Q is stored by row pairs (q_index) so that K3 reads each of its two
         // rows' values as one 16-B piece per bin, contiguous across the wave (a
         // column-major Q made K3's 16-B gathers cost it 4 of its 7 us/frame at
@@ -1601,7 +1619,7 @@ template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
             int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, const float2 *__restrict__ ktab,
-            const float *__restrict__ kmsum, int nframes_blk0, int tail_blocks, int ktail)
+            const float *__restrict__ kmsum, int stg_c2, int nframes_blk0, int tail_blocks, int ktail)
 {
     // Blocks nb .. nb + tail_blocks - 1 (tail_blocks <= nb / 2) are tails: the
     // last ktail frames of the columns of second-half block nb/2 + i, which
@@ -1617,13 +1635,15 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
     // are merged in one L2 (split over XCDs they left as partial-line writes)
     const int blk = xcd_remap(p, nb);
     if (blk == 0) {   // the packed block stops nframes_blk0 frames in (k_cols_tail)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, kmsum, blk, nb);
+        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, kmsum, stg_c2,
+                                       blk, nb);
     } else {
         const int f0 = tail ? nframes - ktail : 0;
         const int nf = tail ? ktail : (p >= nb / 2 && p - nb / 2 < tail_blocks ? nframes - ktail : nframes);
         k_cols_body<LOG2N, MODE, false>(G + (size_t)f0 * g_stride, g_stride,
                                         tail ? G + (size_t)(f0 - 1) * g_stride : Gprev,
-                                        Q + (size_t)f0 * q_stride, q_stride, nf, g, sp, tw, ktab, kmsum, blk, nb);
+                                        Q + (size_t)f0 * q_stride, q_stride, nf, g, sp, tw, ktab, kmsum, stg_c2,
+                                        blk, nb);
     }
 }
 
@@ -1639,11 +1659,12 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
 template <int LOG2N, int MODE>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, int f0, Geo g, Spec sp,
-                 const c2 *__restrict__ tw, const float2 *__restrict__ ktab, const float *__restrict__ kmsum)
+                 const c2 *__restrict__ tw, const float2 *__restrict__ ktab, const float *__restrict__ kmsum,
+                 int stg_c2)
 {
     const int fr = f0 + (int)blockIdx.x;   // >= 1
     k_cols_body<LOG2N, MODE, true>(G + (size_t)fr * g_stride, g_stride, G + (size_t)(fr - 1) * g_stride,
-                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, kmsum, 0);
+                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, kmsum, stg_c2, 0);
 }
 
 // K2's per-bin tables of every column in LDS slot order ([N/2+1][k2_tab_slots]):

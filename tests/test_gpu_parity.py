@@ -454,3 +454,48 @@ def test_k2_tail_bitwise_equals_single_launch(W, H, n, batch, tail, monkeypatch)
     b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+# ---- round 4: K2 staging area and the two-band op -----------------------------
+@pytest.mark.parametrize("W,H,n,batch", [(1920, 1080, 40, 20), (640, 360, 30, 10), (200, 120, 20, 7)])
+def test_k2_dedicated_staging_bitwise_equals_aliased(W, H, n, batch, monkeypatch):
+    """k_cols with its own Q staging area in LDS (2 barriers per frame fewer,
+    where it fits beside two workgroups per CU) gives bitwise the outputs of
+    the staging that aliases the FFT exchange buffers (MM_K2_STGD=0)."""
+    fr = T.synth(W, H, n, fmt="u8")
+    monkeypatch.setenv("MM_K2_STGD", "0")
+    a = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
+    monkeypatch.delenv("MM_K2_STGD")
+    b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("W,H,S", [(256, 192, 25.0), (320, 200, 9.7)])
+def test_two_band_op_l6_vs_oracle(W, H, S):
+    """L = 6 (neighbouring middle bands overlap: MM_K2_PYR_TAB2, the branch-
+    free two-band op) against the oracle's per-level loop at the §8c bars,
+    frame calls and one stream call."""
+    fr = T.synth(W, H, 5)
+    ref = T.oracle_run(W, H, fr, 6, S)
+    for mode in ("frame", "stream"):
+        got = T.gpu_run(W, H, fr, 6, S, mode=mode, batch=3)
+        assert np.array_equal(got[0], fr[0])
+        for k in range(1, 5):
+            T.assert_close_f32(got[k], ref[k], integer_scale=float(S).is_integer())
+
+
+def test_two_band_op_tail_and_batch_bitwise(monkeypatch):
+    """The two-band kernel across launch shapes: 1080p L = 6, a 30-frame
+    stream in one batch without and with k_cols_tail (40 %: the packed
+    block's last 12 frames) and in one-frame calls, all bitwise equal."""
+    W, H = 1920, 1080
+    fr = T.synth(W, H, 30, fmt="u8")
+    monkeypatch.setenv("MM_K2_TAIL", "0")
+    a = T.gpu_run(W, H, fr, 6, 25.0, mode="stream", batch=30)
+    monkeypatch.setenv("MM_K2_TAIL", "40")
+    b = T.gpu_run(W, H, fr, 6, 25.0, mode="stream", batch=30)
+    monkeypatch.delenv("MM_K2_TAIL")
+    c = T.gpu_run(W, H, fr, 6, 25.0, mode="frame", batch=1)
+    for x, y, z in zip(a, b, c):
+        assert np.array_equal(x, y) and np.array_equal(x, z)

@@ -6,7 +6,8 @@ under-reads wide streaming loads (MI355X_MICROARCH.md §HBM); each counter is
 corrected by the factor measured on tools/pmc_calib (512 MiB streamed at the
 access width that dominates the kernel's traffic).
 
-usage: pmc_summary.py FETCH_DIR WRITE_DIR CAL_FETCH_DIR CAL_WRITE_DIR FRAMES_PER_LAUNCH OUT
+usage: pmc_summary.py FETCH_DIR WRITE_DIR CAL_FETCH_DIR CAL_WRITE_DIR FRAMES_PER_LAUNCH OUT [CONFIG]
+(CONFIG: bench.profile_key of the measured configuration, stored as "config")
 """
 import csv
 import glob
@@ -47,6 +48,7 @@ def read_counter(d, counter):
 
 def main():
     fdir, wdir, cfdir, cwdir, fpl, out = sys.argv[1:7]
+    config = sys.argv[7] if len(sys.argv) > 7 else None
     fpl = int(fpl)
     fetch, write = read_counter(fdir, "FETCH_SIZE"), read_counter(wdir, "WRITE_SIZE")
     cfetch, cwrite = read_counter(cfdir, "FETCH_SIZE"), read_counter(cwdir, "WRITE_SIZE")
@@ -66,6 +68,8 @@ def main():
     res = {"frames_per_launch": fpl, "calibration": {"fetch_factor": fcorr, "write_factor": wcorr},
            "kernels": kernels,
            "frame_hbm_bytes": sum(v["hbm_bytes_per_frame"] for v in kernels.values())}
+    if config:
+        res["config"] = config
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

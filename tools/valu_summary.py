@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU issue utilisation per kernel from rocprofv3 PMC + kernel-trace runs.
 
-usage: valu_summary.py PMC_DIR[,PMC_DIR...] KERNEL_TRACE_DIR OUT_JSON
+usage: valu_summary.py PMC_DIR[,PMC_DIR...] KERNEL_TRACE_DIR OUT_JSON [CONFIG]
 
 valu_busy = SQ_INSTS_VALU * 4 cycles / (SIMDs * kernel cycles), with the
 kernel's cycles from its average kernel-trace duration and the shader clock
@@ -57,6 +57,8 @@ for k, c in pmc.items():
               "launch_s": t, "clock_GHz": round(clk / 1e9, 3),
               "valu_busy": round(valu * 4 / (SIMDS * clk * t), 3),
               "valu_busy_peak_clk": round(valu * 4 / (SIMDS * 2.4e9 * t), 3)}
+if len(sys.argv) > 4:
+    out["config"] = sys.argv[4]   # bench.profile_key of the measured configuration
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 for k, v in sorted(out.items()):
     print(k, v)
