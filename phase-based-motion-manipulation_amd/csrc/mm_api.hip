@@ -1523,6 +1523,11 @@ int mm_debug_k2_entry(unsigned long long *host, int n)
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(mm_k2_entry), sizeof(unsigned long long) * n) == hipSuccess
                ? MM_OK : MM_ERR_HIP;
 }
+int mm_debug_k2_exit(unsigned long long *host, int n)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(mm_k2_exit), sizeof(unsigned long long) * n) == hipSuccess
+               ? MM_OK : MM_ERR_HIP;
+}
 #endif
 
 }  // extern "C"

@@ -1050,6 +1050,7 @@ template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes()
 // (s_memtime deltas), written by lane 0 with a vector store after the loop.
 __device__ unsigned long long mm_k2_stamps[4096 * 8 * 8];
 __device__ unsigned long long mm_k2_entry[4096 * 8];   // s_memrealtime at entry, per wave
+__device__ unsigned long long mm_k2_exit[4096 * 8];    // ... after the last Q stores completed (vmcnt 0)
 #define K2_STAMP(i)                                                      \
     do {                                                                 \
         const unsigned long long n_ = __builtin_amdgcn_s_memtime();      \
@@ -1601,12 +1602,15 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     }
 #ifdef MM_K2_STAMPS
     st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
+    __builtin_amdgcn_s_waitcnt(0);   // every load and store of the wave completed
+    const unsigned long long st_exit = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x % 64 == 0) {
         // k_cols_tail's workgroups (one per frame) after k_cols's 4096 waves
         const int w = (blk0 && nframes == 1 && gridDim.x < 512 ? 4096 : 0) +
                       blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
         for (int i = 0; i < 8; ++i) mm_k2_stamps[w * 8 + i] = st_acc[i];
         mm_k2_entry[w] = st_entry;
+        mm_k2_exit[w] = st_exit;
     }
 #endif
 }
@@ -1982,19 +1986,31 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
     st_acc[7] = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (int s = 0; s < steps; ++s) {
-        // ---- K3 on list-row pair i0/2 + 2s + grp (zero beyond Hn) ----
-        const int ka = i0 + 4 * s + 2 * grp;
-        const bool valid = ka < g.Hn;
-        const int kl = valid ? ka : 0;
+    // Q rows of step s: list-row pair i0/2 + 2s + grp (zero beyond Hn).
+    // The compose runs two output rows at a time (4 chroma rows live, not 6:
+    // 128 -> 120 VGPRs).  MM_K34_QPF=1 (diagnostic) issues step s+1's Q loads
+    // after step s's blur, to land under its compose: +32 live VGPRs, 120 B
+    // of spills at the 128-VGPR bound (4 waves per SIMD), so off by default.
+    float4 qv[8];
+    auto load_q = [&](int s_) {
+        const int ka_ = i0 + 4 * s_ + 2 * grp;
+        const int kl = ka_ < g.Hn ? ka_ : 0;
         const float4 *Qp = reinterpret_cast<const float4 *>(Qf + (size_t)(kl / TK) * g.Qs * TK + (kl % TK));
-        float4 qv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int fq = t + j * T;
             const int ff = fq > N / 2 ? N - fq : fq;
             qv[j] = Qp[(size_t)ff * (TK / 2)];
         }
+    };
+#ifndef MM_K34_QPF
+#define MM_K34_QPF 0
+#endif
+    if (MM_K34_QPF) load_q(0);
+    for (int s = 0; s < steps; ++s) {
+        const int ka = i0 + 4 * s + 2 * grp;
+        const bool valid = ka < g.Hn;
+        if (!MM_K34_QPF) load_q(s);
         c2 v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -2036,13 +2052,16 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         }
         __syncthreads();   // LDS free for the next step's FFT
         K34_STAMP(3);
+        if (MM_K34_QPF && s + 1 < steps) load_q(s + 1);
         if (s > 0) {
-            // ---- K4 on output rows i0+4s-4 .. i0+4s-1 ----
-#pragma unroll
-            for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
-            K34_STAMP(4);
+            // ---- K4 on output rows i0+4s-4 .. i0+4s-1, two at a time ----
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+                if (r % 2 == 0) {
+                    chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
+                    chroma_row(i0 + 4 * s - 2 + r, hc[3 + r]);
+                }
+                K34_STAMP(4);
                 const int i = i0 + 4 * s - 4 + r;
                 if (vq && i < g.H) {
                     const float4 wr = rowW3[i];

@@ -26,8 +26,10 @@ out = torch.empty_like(fr)
 h.synth(fr, 0, n)
 h.process_stream(fr, out, n, mm355.RGBA8)      # warm-up (first frame passthrough)
 torch.cuda.synchronize()
+h.profile_begin()
 h.process_stream(fr, out, n, mm355.RGBA8)      # the launch whose stamps are read
 torch.cuda.synchronize()
+kprof = h.profile_end()                         # HIP events around each launch on its stream
 L = mm355.lib()
 nw = 4096
 buf = (ctypes.c_ulonglong * (nw * 8))()
@@ -63,6 +65,19 @@ if hasattr(L, "mm_debug_k2_entry"):   # kernel entry per wave (100 MHz): dispatc
     e0 = lo - lo.min()
     res["entry_skew_us"] = {q: round(float(np.percentile(e0, q)) / 100.0, 2) for q in (0, 50, 90, 100)}
     res["prologue_us"] = {q: round(float(np.percentile(start - lo, q)) / 100.0, 2) for q in (0, 50, 90, 100)}
+    if hasattr(L, "mm_debug_k2_exit"):   # after each wave's last stores completed (vmcnt 0)
+        xb = (ctypes.c_ulonglong * nw)()
+        L.mm_debug_k2_exit.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        assert L.mm_debug_k2_exit(xb, nw) == 0
+        ex = np.frombuffer(xb, dtype=np.uint64).astype(np.int64) & 0xffffffff
+        ok = (ex > 0) & (lo > 0)
+        # one 100 MHz clock (s_memrealtime) for entry and exit: the span of the
+        # waves' work, first entry to last completed store, against the launch's
+        # HIP-event time (which adds the dispatch and the end-of-kernel release)
+        res["wave_span_us"] = round(float(ex[ok].max() - lo[ok].min()) / 100.0, 2)
+        res["exit_after_loop_us"] = {q: round(float(np.percentile(ex[ok] - (start[ok] + (dur[ok] / 10).astype(np.int64)), q)) / 100.0, 2)
+                                    for q in (0, 50, 100)}
+        res["kernel_event_us"] = {k: round(v[0] * 1e3 / max(v[1], 1), 2) for k, v in kprof.items() if v[1]}
 print(json.dumps(res))
 if len(sys.argv) > 2:
     np.save(sys.argv[2], raw)
