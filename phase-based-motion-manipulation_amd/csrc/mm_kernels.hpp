@@ -986,8 +986,13 @@ template <int LOG2N> constexpr int k2_groups() { return groups_at_least<LOG2N, M
 // r ^ ((r >> 3) & 1).  The row writes of a 16-lane group (every other float4
 // of a 16-float4 span) then cover all 32 banks once (linear: 2-way), and the
 // ds_read_b128 groups still read 16 distinct 4-bank slots (tools/lds_banks.py).
+#ifndef MM_K2_NOSWZ
 __device__ __forceinline__ int k2_stg_swz(int i) { return i ^ (((i >> 4) & 1) << 1); }
 __device__ __forceinline__ int k2_stg_swz4(int r) { return r ^ ((r >> 3) & 1); }
+#else   // diagnostic: linear staging
+__device__ __forceinline__ int k2_stg_swz(int i) { return i; }
+__device__ __forceinline__ int k2_stg_swz4(int r) { return r; }
+#endif
 template <int LOG2N> constexpr int k2_threads() { return k2_groups<LOG2N>() * fft_T<LOG2N>(); }
 // dynamic LDS of k_cols: per group the FFT exchange buffer and its column's
 // per-bin table, plus for column N/2 (packed group only) its table, its
@@ -2025,7 +2030,11 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         K34_STAMP(0);
         fft_regs<LOG2N, +1>(v, t, lds, tw);
         K34_STAMP(1);
+#ifndef MM_K34_BLUR_R3
         float *raw = reinterpret_cast<float *>(lds) + kZShift;   // [2][N] |z| of rows ka, ka+1
+#else
+        float *raw = reinterpret_cast<float *>(lds);
+#endif
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             raw[t + j * T] = fabsf(v[j].x);
@@ -2040,11 +2049,19 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         // ds_read2_b64 of 8-B aligned halves (2-way conflicts on every one,
         // tools/lds_banks.py "k34"); same expressions and order as k_rows_inv
         // one base address; the rows are immediate offsets
+#ifndef MM_K34_BLUR_R3
         const float4 *b4 = reinterpret_cast<const float4 *>(raw_all) + ((g.x0 + X) >> 2);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float4 *r4 = b4 + ((r >> 1) * GROUP_FLOATS + (r & 1) * N) / 4;
             const float4 P = r4[0], Z = r4[1];   // z[c-2 .. c+1], z[c+2 .. c+5]
+#else   // diagnostic: round 3's unshifted rows (taps read by the compiler's ds_read2_b64)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 *r4 = reinterpret_cast<const float4 *>(raw_all + (r >> 1) * GROUP_FLOATS + (r & 1) * N + g.x0 + X);
+            const float4 A = r4[-1], B = r4[0], C = r4[1];
+            const float4 P = make_float4(A.z, A.w, B.x, B.y), Z = make_float4(B.z, B.w, C.x, C.y);
+#endif
             yw[4 + r][0] = bw.w0 * P.z + bw.w1 * (P.y + P.w) + bw.w2 * (P.x + Z.x);
             yw[4 + r][1] = bw.w0 * P.w + bw.w1 * (P.z + Z.x) + bw.w2 * (P.y + Z.y);
             yw[4 + r][2] = bw.w0 * Z.x + bw.w1 * (P.w + Z.y) + bw.w2 * (P.z + Z.z);
@@ -2056,11 +2073,16 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         if (s > 0) {
             // ---- K4 on output rows i0+4s-4 .. i0+4s-1, two at a time ----
 #pragma unroll
+#ifdef MM_K34_ROWS4   // diagnostic: round 3's order, the 4 chroma rows first
+            for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
+#endif
             for (int r = 0; r < 4; ++r) {
+#ifndef MM_K34_ROWS4
                 if (r % 2 == 0) {
                     chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
                     chroma_row(i0 + 4 * s - 2 + r, hc[3 + r]);
                 }
+#endif
                 K34_STAMP(4);
                 const int i = i0 + 4 * s - 4 + r;
                 if (vq && i < g.H) {

@@ -101,7 +101,7 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
 // band loop issues no loads (twiddle bases hoisted), so its stores are never
 // waited for.
 template <int LOG2N>
-__global__ __launch_bounds__(k2_threads<LOG2N>())
+__global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_stride, Geo g, Spec sp,
                const c2 *__restrict__ tw)
 {
@@ -149,22 +149,32 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     const int nb = nmid * (sp.O / 2);
     const int kx0 = blk * GPW;
     c2 *stg = lds_all;   // [Hn][GPW]
-    for (int b = 0; b <= nb; ++b) {
+    // Bands level-major (b = o nmid + i - 1 as before): the radial mask of a
+    // level is evaluated once for its O/2 orientation bands, which then only
+    // add the angular factor (the same expressions per band: bitwise the
+    // band-major loop's values).  The residual band (b = nb) runs last.
+    float rm[8];
+    for (int lb = 0; lb <= nb; ++lb) {
+        const int i = lb < nb ? 1 + lb / (sp.O / 2) : 0, o = lb < nb ? lb % (sp.O / 2) : 0;
+        const int b = lb < nb ? o * nmid + (i - 1) : nb;
         // opaque lane index and twiddle bases per band: keeps LICM from
         // hoisting the FFT addressing and twiddle powers into live registers
         int t = t0;
         asm volatile("" : "+v"(t));
         c2 wt[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            wt[i] = wtw[i];
-            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
+        for (int q = 0; q < 16; ++q) {
+            wt[q] = wtw[q];
+            if (tw_slot_used(LOG2N, q)) asm volatile("" : "+v"(wt[q]));
         }
-        const int o = nmid ? b / nmid : 0, i = nmid ? 1 + b % nmid : 0;
         // workgroup-uniform: skip the band where all its columns are zero
         bool all_zero = true;
         for (int c = 0; c < GPW && kx0 + c < N; ++c) all_zero &= band_col_zero<N>(b, nb, nmid, kx0 + c, sp);
-        if (all_zero) continue;
+        if (all_zero) continue;   // (then every band of this level: o = 0 skips them all)
+        if (lb < nb && o == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rm[j] = level_mask(fr[j], i, sp);
+        }
         c2 v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -175,7 +185,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
                 const float ao = isum[j] < 0.0f
                                      ? 1.0f / (float)sp.O
                                      : pow4(fmaxf(0.0f, cx[j] * sp.ang_c[o] + sy[j] * sp.ang_s[o])) * isum[j];
-                m = level_mask(fr[j], i, sp) * ao;
+                m = rm[j] * ao;
             }
             v[j] = scale(v0[j], m);
         }

@@ -4,7 +4,7 @@ import sys, os, time, threading
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "phase-based-motion-manipulation_amd"))
 import torch, mm355
-from test_handle import _Gate
+from gate_scenarios import Gate as _Gate
 
 def probe(name, op):
     sb = torch.cuda.Stream()
