@@ -72,7 +72,7 @@ struct mm_handle {
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     bool k2_pow;                // ... and the phase factor as z^S (integer S, MM_K2_PYR_POW)
     bool k2_tab2;               // ... with overlapping middle bands (MM_K2_PYR_TAB2)
-    bool k2_stg_ded;            // k_cols stages Q in its own LDS area where it fits (MM_K2_STGD=0: off)
+    bool k2_stg_ded;            // k_cols stages Q in its own LDS area where it fits (MM_K2_STGD=1)
     uint8_t *d_stage_in, *d_stage_out;
     size_t stage_bytes;
     bool has_state;
@@ -736,10 +736,16 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             HIPCHK(hipGetLastError());
         }
         ProfScope ps(h, s, MM_K_ROWS_INV, reset || !write ? 0 : 1);
-        hipLaunchKernelGGL((k_sb_rows<LOG2N>), dim3((h->geo.Hn + gpw - 1) / gpw),
-                           dim3(wg_threads<LOG2N>()), lds, s, h->d_T, band_stride,
-                           h->d_Yh + h->yh_stride * k, sst, sst + plane, sst + 2 * plane, reset,
-                           write && !reset ? 1 : 0, h->geo, h->spec, h->blur, h->d_tw);
+        if (h->spec.filt == MM_FILTER_IIR)
+            hipLaunchKernelGGL((k_sb_rows<LOG2N, true>), dim3((h->geo.Hn + gpw - 1) / gpw),
+                               dim3(wg_threads<LOG2N>()), lds, s, h->d_T, band_stride,
+                               h->d_Yh + h->yh_stride * k, sst, sst + plane, sst + 2 * plane, reset,
+                               write && !reset ? 1 : 0, h->geo, h->spec, h->blur, h->d_tw);
+        else
+            hipLaunchKernelGGL((k_sb_rows<LOG2N, false>), dim3((h->geo.Hn + gpw - 1) / gpw),
+                               dim3(wg_threads<LOG2N>()), lds, s, h->d_T, band_stride,
+                               h->d_Yh + h->yh_stride * k, sst, sst + plane, sst + 2 * plane, reset,
+                               write && !reset ? 1 : 0, h->geo, h->spec, h->blur, h->d_tw);
         HIPCHK(hipGetLastError());
     }
     if (sst == h->d_sst) h->steer_valid = true;
@@ -1159,7 +1165,9 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
-    h->k2_stg_ded = !(getenv("MM_K2_STGD") && atoi(getenv("MM_K2_STGD")) == 0);
+    // dedicated Q staging: 2 barriers per frame fewer, but same-call K2 +1 %
+    // at 1080p (r04d); opt-in (MM_K2_STGD=1)
+    h->k2_stg_ded = getenv("MM_K2_STGD") && atoi(getenv("MM_K2_STGD")) == 1;
     h->k2_tail2_pct = getenv("MM_K2_TAIL2") ? atoi(getenv("MM_K2_TAIL2")) : 10;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
     h->k34_oneshot = getenv("MM_K34_ONESHOT") ? atoi(getenv("MM_K34_ONESHOT")) : 1;

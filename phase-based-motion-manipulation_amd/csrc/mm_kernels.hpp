@@ -1992,10 +1992,10 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
     st_acc[7] = __builtin_amdgcn_s_memrealtime();
 #endif
     // Q rows of step s: list-row pair i0/2 + 2s + grp (zero beyond Hn).
-    // The compose runs two output rows at a time (4 chroma rows live, not 6:
-    // 128 -> 120 VGPRs).  MM_K34_QPF=1 (diagnostic) issues step s+1's Q loads
-    // after step s's blur, to land under its compose: +32 live VGPRs, 120 B
-    // of spills at the 128-VGPR bound (4 waves per SIMD), so off by default.
+    // MM_K34_QPF=1 (diagnostic) issues step s+1's Q loads after step s's blur,
+    // to land under its compose: +32 live VGPRs, 120 B of spills at the
+    // 128-VGPR bound (4 waves per SIMD) even with the compose two rows at a
+    // time (MM_K34_ROWS2), so off by default.
     float4 qv[8];
     auto load_q = [&](int s_) {
         const int ka_ = i0 + 4 * s_ + 2 * grp;
@@ -2073,11 +2073,11 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         if (s > 0) {
             // ---- K4 on output rows i0+4s-4 .. i0+4s-1, two at a time ----
 #pragma unroll
-#ifdef MM_K34_ROWS4   // diagnostic: round 3's order, the 4 chroma rows first
+#ifndef MM_K34_ROWS2   // the 4 chroma rows' loads first (one memory round trip)
             for (int r = 0; r < 4; ++r) chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
 #endif
             for (int r = 0; r < 4; ++r) {
-#ifndef MM_K34_ROWS4
+#ifdef MM_K34_ROWS2   // diagnostic: two rows at a time (120 VGPRs; same-call K34 +8 %, r04d)
                 if (r % 2 == 0) {
                     chroma_row(i0 + 4 * s - 3 + r, hc[2 + r]);
                     chroma_row(i0 + 4 * s - 2 + r, hc[3 + r]);

@@ -226,8 +226,14 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 // b+1's state loads follow the stores and are consumed only after its FFT,
 // when the stores have long completed.  The pointers are not restrict so
 // that the compiler keeps this order.
-template <int LOG2N>
-__global__ __launch_bounds__(wg_threads<LOG2N>())
+// IIR: the temporal filter as a template parameter, so that the DIFF kernel
+// carries one state plane's registers, not three: 120 VGPRs (3 planes, 4
+// waves per SIMD) -> <= 96 (5 waves per SIMD).  At 1080p the Hn = 1,084 rows
+// are 1,084 four-wave workgroups: at 4 waves per SIMD 1,024 of them run at
+// once and the last 60 make a second round of the whole row time; at 5 they
+// all fit one round.
+template <int LOG2N, bool IIR>
+__global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
                float *st_phi, float *st_uh, float *st_ul,
                int reset, int write_out, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
@@ -242,7 +248,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     const int Wc = g.W + 4, xs = g.x0 - 2;
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
-    const bool iir = sp.filt == MM_FILTER_IIR;
+    constexpr bool iir = IIR;
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);

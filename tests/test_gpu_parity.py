@@ -459,13 +459,14 @@ def test_k2_tail_bitwise_equals_single_launch(W, H, n, batch, tail, monkeypatch)
 # ---- round 4: K2 staging area and the two-band op -----------------------------
 @pytest.mark.parametrize("W,H,n,batch", [(1920, 1080, 40, 20), (640, 360, 30, 10), (200, 120, 20, 7)])
 def test_k2_dedicated_staging_bitwise_equals_aliased(W, H, n, batch, monkeypatch):
-    """k_cols with its own Q staging area in LDS (2 barriers per frame fewer,
-    where it fits beside two workgroups per CU) gives bitwise the outputs of
-    the staging that aliases the FFT exchange buffers (MM_K2_STGD=0)."""
+    """k_cols with its own Q staging area in LDS (MM_K2_STGD=1: 2 barriers per
+    frame fewer, where it fits beside two workgroups per CU; opt-in) gives
+    bitwise the outputs of the default staging that aliases the FFT exchange
+    buffers."""
     fr = T.synth(W, H, n, fmt="u8")
     monkeypatch.setenv("MM_K2_STGD", "0")
     a = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
-    monkeypatch.delenv("MM_K2_STGD")
+    monkeypatch.setenv("MM_K2_STGD", "1")
     b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=batch)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
