@@ -111,12 +111,17 @@ def profile_key(W, H, L, orientations, standard, filt):
 
 
 def load_profile(name, key):
-    path = os.path.join(ROOT, "profiles", name)
-    try:
-        d = json.load(open(path))
-    except Exception:
-        return None
-    return d if d.get("config") == key else None
+    """profiles/NAME (the default configuration's) or profiles/<stem>_<key>.json,
+    whichever records `key` as its measured configuration; else None."""
+    stem = name[:-5] if name.endswith(".json") else name
+    for fn in (f"{stem}_{key}.json", name):
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", fn)))
+        except Exception:
+            continue
+        if d.get("config") == key:
+            return d
+    return None
 
 
 def parse(argv=None):

@@ -19,7 +19,11 @@ from collections import defaultdict
 
 # dominant (read width, write width) in bytes per lane, per kernel
 WIDTHS = {"k_rows_fwd": (4, 16), "k_cols": (8, 8), "k_rows_inv": (16, 4), "k_compose": (4, 4),
-          "k_rows_inv_compose": (16, 16)}
+          "k_rows_inv_compose": (16, 16),
+          # steerable extension (mm_steer.hpp): k_cols_fwd once per batch, the
+          # band kernels once per frame
+          "k_cols_fwd": (8, 8), "k_sb_cols": (8, 16), "k_sb_rows": (8, 4)}
+PER_FRAME = {"k_sb_cols", "k_sb_rows"}
 CAL_BYTES = 512 << 20
 
 
@@ -63,11 +67,19 @@ def main():
         kernels[k] = {"fetch_bytes_raw": fb, "write_bytes_raw": wb,
                       "fetch_bytes": fc, "write_bytes": wc,
                       "hbm_bytes_per_launch": fc + wc,
-                      "hbm_bytes_per_frame": (fc + wc) / fpl,
+                      "hbm_bytes_per_frame": (fc + wc) / (1 if k in PER_FRAME else fpl),
                       "read_width": rw, "write_width": ww}
+    if "k_sb_cols" in kernels and "k_cols_fwd" in kernels:
+        # bench.py's kernel ids (mm_profile_end) of the steerable path: k_cols =
+        # k_cols_fwd + k_sb_cols, k_rows_inv = k_sb_rows
+        kernels["k_cols"] = {"hbm_bytes_per_frame": kernels["k_cols_fwd"]["hbm_bytes_per_frame"] +
+                             kernels["k_sb_cols"]["hbm_bytes_per_frame"], "of": ["k_cols_fwd", "k_sb_cols"]}
+    if "k_sb_rows" in kernels:
+        kernels["k_rows_inv"] = {"hbm_bytes_per_frame": kernels["k_sb_rows"]["hbm_bytes_per_frame"],
+                                 "of": ["k_sb_rows"]}
     res = {"frames_per_launch": fpl, "calibration": {"fetch_factor": fcorr, "write_factor": wcorr},
            "kernels": kernels,
-           "frame_hbm_bytes": sum(v["hbm_bytes_per_frame"] for v in kernels.values())}
+           "frame_hbm_bytes": sum(v["hbm_bytes_per_frame"] for k, v in kernels.items() if "of" not in v)}
     if config:
         res["config"] = config
     json.dump(res, open(out, "w"), indent=1)
