@@ -37,6 +37,7 @@ import os
 import sys
 
 import numpy as np
+from scipy import fft as sfft
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "tests"))
@@ -44,6 +45,8 @@ import np_twin as T  # noqa: E402
 
 FILTER_DIFF = 0
 FILTER_IIR = 1
+# threads of the float64 FFTs (scipy.fft workers); the 2160p case sets 16
+WORKERS = 1
 
 
 def angular_masks(N, O):
@@ -82,35 +85,54 @@ class SteerableRef:
         m = T.masks(self.N, levels, min_freq, max_freq)
         self.res = m[0] + (m[-1] if levels > 1 else 0)
         a = angular_masks(self.N, orientations)
-        self.bands = [m[i] * a[o] for i in range(1, levels - 1) for o in range(orientations // 2)]
+        self.bands = [(i, o) for i in range(1, levels - 1) for o in range(orientations // 2)]
+        self.m, self.a = m, a
         self.state = None
 
-    def _subbands(self, F):
-        return [np.fft.ifft2(np.fft.ifftshift(F * b)) for b in self.bands]
+    def _ifft2c(self, X):
+        return sfft.ifft2(sfft.ifftshift(X), workers=1 if WORKERS > 1 else None)
+
+    def _band(self, F, i, o, st):
+        """One subband: (2 Re s', its new state), or the first frame's state."""
+        s = self._ifft2c(F * (self.m[i] * self.a[o]))
+        ph = np.arctan2(s.imag, s.real)
+        if st is None:
+            z = np.zeros(s.shape) if self.filt == FILTER_IIR else None
+            return None, (ph, z, None if z is None else z.copy())
+        ph_prev, uh, ul = st
+        if self.filt == FILTER_DIFF:
+            P = T.wrap_phase(ph_prev - ph)
+        else:
+            d = T.wrap_phase(ph - ph_prev)
+            uh = (1.0 - self.rh) * (uh + d)
+            ul = (1.0 - self.rl) * (ul + d)
+            P = ul - uh
+        # Re(s e^{i S P}) where |s| >= tau, Re(s) elsewhere
+        SP = self.S * P
+        re = np.where(np.hypot(s.real, s.imag) < self.tau, s.real, s.real * np.cos(SP) - s.imag * np.sin(SP))
+        return 2.0 * re, (ph, uh, ul)
 
     def process(self, frame):
-        """frame: float RGBA [H, W, 4] in [0, 1]; returns the output frame."""
+        """frame: float RGBA [H, W, 4] in [0, 1]; returns the output frame.
+        The subbands are formed one per task (the 2160p, O = 8 case holds 16
+        of them: 4 GB at once otherwise), WORKERS tasks at a time."""
         pc = T.pad_window(frame.astype(np.float64), self.N, self.edge)
-        F = np.fft.fftshift(np.fft.fft2(pc[..., 0]))
-        sb = self._subbands(F)
-        if self.state is None:                      # first frame: passthrough
-            self.state = [(np.angle(s), np.zeros(s.shape), np.zeros(s.shape)) for s in sb]
+        F = sfft.fftshift(sfft.fft2(pc[..., 0], workers=WORKERS))
+        first = self.state is None
+        prev = [None] * len(self.bands) if first else self.state
+        jobs = [(i, o, st) for (i, o), st in zip(self.bands, prev)]
+        if WORKERS > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(WORKERS) as ex:
+                res = list(ex.map(lambda j: self._band(F, *j), jobs))
+        else:
+            res = [self._band(F, *j) for j in jobs]
+        self.state = [r[1] for r in res]
+        if first:                                   # first frame: passthrough
             return frame.copy()
-        y = np.real(np.fft.ifft2(np.fft.ifftshift(F * self.res)))
-        new_state = []
-        for s, (ph_prev, uh, ul) in zip(sb, self.state):
-            ph = np.angle(s)
-            if self.filt == FILTER_DIFF:
-                P = T.wrap_phase(ph_prev - ph)
-            else:
-                d = T.wrap_phase(ph - ph_prev)
-                uh = (1.0 - self.rh) * (uh + d)
-                ul = (1.0 - self.rl) * (ul + d)
-                P = ul - uh
-            sp = np.where(np.abs(s) < self.tau, s, s * np.exp(1j * self.S * P))
-            y = y + 2.0 * np.real(sp)
-            new_state.append((ph, uh, ul))
-        self.state = new_state
+        y = np.real(self._ifft2c(F * self.res))
+        for r in res:
+            y = y + r[0]
         rgb, _ = finish(pc, np.abs(y), self.edge)
         N, W, H = self.N, self.W, self.H
         tx = ((N - W) + 2 * np.arange(W)) / 2.0
