@@ -70,7 +70,7 @@ struct mm_handle {
     hipEvent_t retire_ev;       // orders a buffer's return to the pool behind a call's stream
     bool last_ev_set;
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
-    bool k2_pow;                // ... and the phase factor as z^S (integer S, MM_K2_PYR_POW)
+    int k2_sp;                  // ... and the phase factor as z^S, |S| == k2_sp (k_cols SP; 0: atan2)
     bool k2_tab2;               // ... with overlapping middle bands (MM_K2_PYR_TAB2)
     bool k2_stg_ded;            // k_cols stages Q in its own LDS area where it fits (MM_K2_STGD=1)
     uint8_t *d_stage_in, *d_stage_out;
@@ -79,6 +79,7 @@ struct mm_handle {
     bool g_valid;               // the G slot gs holds G_{t-1} (K1 or a non-steerable mm_set_state
                                 // wrote it; a steerable mm_set_state sets only the local phases)
     int k2_tail_pct;            // share of a batch's frames of k_cols's packed block run by k_cols_tail
+    bool k2_pk_all;             // ... all of them (batches >= 24 frames): block 0 leaves k_cols
     int k2_tail2_pct;           // share of the second-half blocks' frames run by k_cols's tail blocks
     int k34_rows;               // output rows per k_rows_inv_compose strip (0: K3 + K4 unfused;
                                 // -1: by the launch's frame count, k34_strip_rows)
@@ -317,6 +318,16 @@ static bool bands_overlap(const Spec &sp)
     return false;
 }
 
+// k_cols' power-form instance for this handle (mm_kernels.hpp cpow_x2): |S|
+// for an integer phase scale with a compiled instance (|S| 25 and 10, the
+// configurations' values, at N >= 2048), else 0 (the atan2 form).
+// MM_K2_POW=0 selects the atan2 form throughout.
+static int k2_power_exponent(const Spec &sp, int N)
+{
+    if (getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW")) == 0) return 0;
+    return N >= 2048 && (sp.S_pow == 25 || sp.S_pow == 10) ? sp.S_pow : 0;
+}
+
 // GaussianBlur.shader:47-60 at _BlurSize 0.5 (.cs:427): bilinear taps at
 // +-0.6923 and +-1.6154 texels == a 5-tap FIR.
 static Blur5 build_blur()
@@ -454,31 +465,44 @@ static int launch_k2(mm_handle *h, int nframes, const c2 *Gprev, const c2 *G, hi
         h->ktab_mode = tab_mode;
     }
     ProfScope ps(h, s, MM_K_COLS, nframes);
-    // the packed block's last k frames go to k_cols_tail (k_cols's critical path)
+    // the packed block's last k frames go to k_cols_tail (k_cols's critical
+    // path); all of them (k = nframes, block 0 not in k_cols) where
+    // k2_pk_all is set: k_cols's LDS then omits the packed group's arrays
+    const bool pk_all = h->k2_pk_all && nframes >= 24 && blocks >= 2;
     int k = nframes >= 24 ? nframes * h->k2_tail_pct / 100 : 0;
-    k = std::max(0, std::min(k, nframes - 2));
+    k = pk_all ? nframes : std::max(0, std::min(k, nframes - 2));
+    const int pk_off = pk_all ? 1 : 0, cb = blocks - pk_off;   // column blocks of k_cols
     // second-half tails (k_cols): the last k2 frames of each second-half block's
     // columns in extra blocks (MM_K2_TAIL2 percent)
-    const int k2t = nframes >= 24 && blocks >= 2 ? std::min(nframes * h->k2_tail2_pct / 100, nframes - 2) : 0;
-    const int tb = k2t > 0 ? blocks / 2 : 0;
-#define MM_K2_LAUNCH(MODE)                                                                           \
+    const int k2t = nframes >= 24 && cb >= 2 ? std::min(nframes * h->k2_tail2_pct / 100, nframes - 2) : 0;
+    const int tb = k2t > 0 ? cb / 2 : 0;
+#define MM_K2_LAUNCH(MODE, SP)                                                                       \
     do {                                                                                             \
-        const int sc2 = h->k2_stg_ded ? k2_stg_c2<LOG2N, MODE>(h->geo.Hq) : 0; /* dedicated staging */ \
-        /* (dedicated staging +) exchange buffers + per-bin tables */                               \
-        const size_t lds = k2_lds_bytes<LOG2N, MODE>() + sizeof(c2) * (size_t)sc2;                   \
-        hipLaunchKernelGGL((k_cols<LOG2N, MODE>), dim3(blocks + tb), dim3(k2_threads<LOG2N>()), lds, s, G, \
+        const int sc2 = h->k2_stg_ded ? k2_stg_c2<LOG2N, MODE>(h->geo.Hq, !pk_all) : 0; /* dedicated staging */ \
+        /* (dedicated staging +) exchange buffers + per-bin tables (+ the packed group's) */       \
+        const size_t lds = k2_lds_bytes<LOG2N, MODE>(!pk_all) + sizeof(c2) * (size_t)sc2;           \
+        hipLaunchKernelGGL((k_cols<LOG2N, MODE, SP>), dim3(cb + tb), dim3(k2_threads<LOG2N>()), lds, s, G, \
                            h->g_stride, Gprev, h->d_Q, h->q_stride, nframes, h->geo, h->spec, h->d_tw, h->d_ktab, \
-                           h->d_kmsum, sc2, nframes - k, tb, k2t);                                   \
-        if (k)                                                                                       \
-            hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE>), dim3(k), dim3(k2_threads<LOG2N>()), lds, s, G, \
-                               h->g_stride, h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab, \
-                               h->d_kmsum, sc2);                                                     \
+                           h->d_kmsum, sc2, nframes - k, tb, k2t, pk_off);                           \
+        if (k) {                                                                                     \
+            const int sct = h->k2_stg_ded ? k2_stg_c2<LOG2N, MODE>(h->geo.Hq) : 0;                  \
+            const size_t ldt = k2_lds_bytes<LOG2N, MODE>() + sizeof(c2) * (size_t)sct;              \
+            hipLaunchKernelGGL((k_cols_tail<LOG2N, MODE, SP>), dim3(k), dim3(k2_threads<LOG2N>()),  \
+                               ldt, s, G, h->g_stride, Gprev,                                       \
+                               h->d_Q, h->q_stride, nframes - k, h->geo, h->spec, h->d_tw, h->d_ktab,   \
+                               h->d_kmsum, sct);                                                     \
+        }                                                                                            \
     } while (0)
-    if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD);
-    else if (h->k2_tab && h->k2_pow) MM_K2_LAUNCH(MM_K2_PYR_POW);
-    else if (h->k2_tab2) MM_K2_LAUNCH(MM_K2_PYR_TAB2);
-    else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB);
-    else MM_K2_LAUNCH(MM_MODE_PYRAMID);
+    // the power-form instances (k2_power_exponent): 1080p and 2160p, |S| 25, 10
+    constexpr bool pow_ok = LOG2N >= 11;
+    if (h->spec.mode == MM_MODE_STANDARD) MM_K2_LAUNCH(MM_MODE_STANDARD, 0);
+    else if (pow_ok && h->k2_tab2 && h->k2_sp == 25) MM_K2_LAUNCH(MM_K2_PYR_TAB2, (pow_ok ? 25 : 0));
+    else if (pow_ok && h->k2_tab2 && h->k2_sp == 10) MM_K2_LAUNCH(MM_K2_PYR_TAB2, (pow_ok ? 10 : 0));
+    else if (h->k2_tab2) MM_K2_LAUNCH(MM_K2_PYR_TAB2, 0);
+    else if (pow_ok && h->k2_tab && h->k2_sp == 25) MM_K2_LAUNCH(MM_K2_PYR_TAB, (pow_ok ? 25 : 0));
+    else if (pow_ok && h->k2_tab && h->k2_sp == 10) MM_K2_LAUNCH(MM_K2_PYR_TAB, (pow_ok ? 10 : 0));
+    else if (h->k2_tab) MM_K2_LAUNCH(MM_K2_PYR_TAB, 0);
+    else MM_K2_LAUNCH(MM_MODE_PYRAMID, 0);
 #undef MM_K2_LAUNCH
     HIPCHK(hipGetLastError());
     return MM_OK;
@@ -729,8 +753,8 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         const int reset = k < seed;
         {
             ProfScope ps(h, s, MM_K_COLS, 0);
-            const int g2 = k2_groups<LOG2N>();
-            hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(k2_threads<LOG2N>()),
+            const int g2 = sb_groups<LOG2N>();
+            hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),
                                sizeof(c2) * (size_t)g2 * lds_complex<N>(), s, h->d_Fb + fstride * k,
                                h->d_T, band_stride, h->geo, h->spec, h->d_tw);
             HIPCHK(hipGetLastError());
@@ -1160,11 +1184,14 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     g.edge = p->edge_mode;
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
-    h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
+    h->k2_sp = k2_power_exponent(h->spec, h->N);
     h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
     h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
+    // N = 4096 (one-column workgroups, k2_groups): k_cols fits two workgroups
+    // per CU only without the packed group's LDS arrays (MM_K2_PKALL 0 / 1)
+    h->k2_pk_all = getenv("MM_K2_PKALL") ? atoi(getenv("MM_K2_PKALL")) != 0 : N >= 4096;
     // dedicated Q staging: 2 barriers per frame fewer, but same-call K2 +1 %
     // at 1080p (r04d); opt-in (MM_K2_STGD=1)
     h->k2_stg_ded = getenv("MM_K2_STGD") && atoi(getenv("MM_K2_STGD")) == 1;
@@ -1245,7 +1272,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     h->geo.edge = p->edge_mode;
     build_spec(*p, h->N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
-    h->k2_pow = h->spec.S_pow >= 0 && getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW"));
+    h->k2_sp = k2_power_exponent(h->spec, h->N);
     h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
     h->ktab_mode = -1;
     if (edge_changed) return upload_tables(h);

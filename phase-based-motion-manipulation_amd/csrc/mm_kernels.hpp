@@ -53,7 +53,7 @@ struct Spec {
     int L;
     float minF, maxF, S, tau2, inv_nn;
     float S_rev;            // S / (2 pi): phase scale in revolutions (v_sin/v_cos)
-    int S_pow;              // |S| when S is an integer (MM_K2_PYR_POW: e^{i S delta} = z^|S|)
+    int S_pow;              // |S| when S is an integer, else -1 (k_cols SP: the power form)
     float S_sgn;            // sign of S (+1 / -1) for the power form
     float tau2_nn;          // tau2 * inv_nn^2 (gate on masks pre-scaled by inv_nn)
     float hp_lo, hp_inv;    // high-pass ramp start maxF*0.8, 1/(maxF*0.2)
@@ -612,19 +612,6 @@ __device__ __forceinline__ c2 spectral_op(c2 c, c2 p, int fx, int fy, const Spec
 //     The host checks that no 3 bands overlap.
 //   MM_MODE_STANDARD: (w, 0), w = calculate_bandpass_weight (:74-122).
 constexpr int MM_K2_PYR_TAB = 2;
-// MM_K2_PYR_POW: MM_K2_PYR_TAB for an integer phase scale S.  The phase
-// factor of a magnified bin is then a power instead of atan2 + sin/cos:
-//   e^{i S wrap(arg p - arg c)} = e^{i S (arg p - arg c)} = z^S,
-//   z = p conj(c) / (|p| |c|)
-// (wrap subtracts a multiple of 2 pi, which an integer S maps to a multiple
-// of 2 pi: PyramidPhaseDifference.compute:47-54, 92-98).  z^|S| by square and
-// multiply over the bits of |S| (a uniform scalar loop), conj for S < 0.
-// Same value up to fp32 rounding (tests/test_k2_pow.py, against the atan2
-// form and the oracle's atan2f path); non-integer S keeps the atan2 form.
-// Opt-in (MM_K2_POW=1): same-call 4 % slower than the atan2 form in spite of
-// fewer issue slots (the scalar bit loop and its phi moves break the bins'
-// interleaving; profiles/r03_ab3.txt).
-constexpr int MM_K2_PYR_POW = 3;
 // MM_K2_PYR_TAB2: MM_K2_PYR_TAB for band layouts whose neighbouring middle
 // bands overlap (L = 6 at the default 0.05 / 0.45: the C3 configuration).
 // Waves holding a two-band bin run pyramid_op_2band_x2 (branch-free, the
@@ -634,7 +621,7 @@ constexpr int MM_K2_PYR_POW = 3;
 constexpr int MM_K2_PYR_TAB2 = 4;
 template <int MODE> constexpr bool k2_tabled()
 {
-    return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_POW || MODE == MM_K2_PYR_TAB2;
+    return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_TAB2;
 }
 template <int MODE> constexpr bool k2_msum() { return MODE == MM_K2_PYR_TAB2; }
 template <int MODE> constexpr bool k2_one_band_op() { return MODE == MM_K2_PYR_TAB || MODE == MM_K2_PYR_TAB2; }
@@ -885,60 +872,85 @@ __device__ __forceinline__ c2 pyramid_op_2band(c2 c, c2 p, const Spec &sp, float
     return mul(c, mk(mmag * cw + mpass, mmag * sw));
 }
 
-// pyramid_op_1band in the power form (MM_K2_PYR_POW) for NB bins at once (their
-// squarings interleave): v[j] <- c w, prev[j] <- c for j = j0 .. j0 + NB - 1,
-// w = mpass + mmag z^S, the same gate and masks as pyramid_op_1band.
-template <int NB>
-__device__ __forceinline__ void pyramid_op_pow(c2 (&v)[8], c2 (&prev)[8], int j0, const float2 (&mt)[NB],
-                                               const Spec &sp)
+// The power form of the phase factor (k_cols SP > 0: an integer phase scale
+// S with |S| == SP fixed at compile time).  For an integer S
+//   e^{i S wrap(arg p - arg c)} = e^{i S (arg p - arg c)} = z^S,
+//   z = p conj(c) / (|p| |c|)
+// (wrap subtracts a multiple of 2 pi, which an integer S maps to a multiple of
+// 2 pi: PyramidPhaseDifference.compute:47-54, 92-98), so the atan2 polynomial,
+// its octant logic and sin / cos become one rsq and a fixed chain of complex
+// squarings and products, two bins per packed op: |S| = 25 is 4 squarings + 2
+// products, 10 is 3 + 1.  S < 0: conj(z)^|S| (the sign on z's imaginary part).
+// Same value up to fp32 rounding (tests/test_k2_pow.py against the atan2 form
+// and the oracle).  Range: |p| |c| < 2^64 (the product of the squared norms is
+// scaled by 2^-64 before the rsq; any RGBA8 frame is below 2^25 per bin), and
+// a bin with |p|^2 |c|^2 < 2^-62 gets z = u 2^31 instead of u / |u| (such a bin
+// is gated unless tau < 2^-31 / (m N M)).
+
+// (x + i y)^E for two bins at once (one per lane of x and y)
+template <int E>
+__device__ __forceinline__ void cpow_x2(c2 &x, c2 &y)
 {
-    c2 z[NB], r[NB];
-    float mmag[NB], mpass[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const c2 c = v[j0 + b], p = prev[j0 + b];
-        const float cn = c.x * c.x + c.y * c.y, pn = p.x * p.x + p.y * p.y;
-        float mn2;   // min without fminf's NaN canonicalisation (finite operands)
-        asm("v_min_f32 %0, %1, %2" : "=v"(mn2) : "v"(cn), "v"(pn));
-        mmag[b] = mt[b].x * mt[b].x * mn2 < sp.tau2_nn ? 0.0f : mt[b].x;
-        mpass[b] = -mt[b].y - mmag[b];
-        // z = u / |u|, |u|^2 = |p|^2 |c|^2 (a zero bin gives z = 0: finite, and
-        // gated there); plain C: the rsq result feeds this multiply
-        const c2 u = mul_conj(p, c);
-        z[b] = u * __builtin_amdgcn_rsqf(fmaxf(cn * pn, 1e-30f));
-    }
-    // r = z^|S|, square and multiply from the lowest set bit (no multiply by
-    // 1): |S| = 25 takes 4 squarings + 2 products, 10 takes 3 + 1.  The bit
-    // loops are uniform (scalar branches only).
-    int e = sp.S_pow;
-    if (e == 0) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) r[b] = mk(1.0f, 0.0f);
-    } else {
-        for (; !(e & 1); e >>= 1) {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) z[b] = mul(z[b], z[b]);
-        }
-#pragma unroll
-        for (int b = 0; b < NB; ++b) r[b] = z[b];
-        for (e >>= 1; e; e >>= 1) {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) z[b] = mul(z[b], z[b]);
-            if (e & 1) {
-#pragma unroll
-                for (int b = 0; b < NB; ++b) r[b] = mul(r[b], z[b]);
-            }
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const c2 c = v[j0 + b];
-        const c2 w = mk(mmag[b] * r[b].x + mpass[b], (mmag[b] * sp.S_sgn) * r[b].y);
-        prev[j0 + b] = c;
-        v[j0 + b] = mul(c, w);
+    static_assert(E >= 1, "exponent");
+    if constexpr (E % 2 == 0) {
+        cpow_x2<E / 2>(x, y);
+        const c2 xx = x * x - y * y, yy = (x + x) * y;
+        x = xx;
+        y = yy;
+    } else if constexpr (E > 1) {
+        c2 rx = x, ry = y;
+        cpow_x2<E - 1>(rx, ry);
+        const c2 xx = rx * x - ry * y, yy = rx * y + ry * x;
+        x = xx;
+        y = yy;
     }
 }
 
+// pyramid_op_1band_x2 (TWO: pyramid_op_2band_x2, with the bins' mask sums
+// ms0, ms1) in the power form, E = |S|
+template <int E, bool TWO>
+__device__ __forceinline__ void pyramid_op_pow_x2(c2 &v0, c2 &p0, float2 mt0, float ms0, c2 &v1, c2 &p1,
+                                                  float2 mt1, float ms1, const Spec &sp)
+{
+    const c2 c0 = v0, c1 = v1;
+    const float cn0 = c0.x * c0.x + c0.y * c0.y, pn0 = p0.x * p0.x + p0.y * p0.y;
+    const float cn1 = c1.x * c1.x + c1.y * c1.y, pn1 = p1.x * p1.x + p1.y * p1.y;
+    const float mn0 = fminf(cn0, pn0), mn1 = fminf(cn1, pn1);
+    float mmag0, mmag1, mpass0, mpass1;
+    if constexpr (TWO) {
+        const float mb0 = fmaxf(mt0.y, 0.0f), mb1 = fmaxf(mt1.y, 0.0f);
+        mmag0 = (mt0.x * mt0.x * mn0 < sp.tau2_nn ? 0.0f : mt0.x) + (mb0 * mb0 * mn0 < sp.tau2_nn ? 0.0f : mb0);
+        mmag1 = (mt1.x * mt1.x * mn1 < sp.tau2_nn ? 0.0f : mt1.x) + (mb1 * mb1 * mn1 < sp.tau2_nn ? 0.0f : mb1);
+        mpass0 = ms0 - mmag0;
+        mpass1 = ms1 - mmag1;
+    } else {
+        mmag0 = mt0.x * mt0.x * mn0 < sp.tau2_nn ? 0.0f : mt0.x;
+        mmag1 = mt1.x * mt1.x * mn1 < sp.tau2_nn ? 0.0f : mt1.x;
+        mpass0 = -mt0.y - mmag0;
+        mpass1 = -mt1.y - mmag1;
+    }
+    const c2 u0 = mul_conj(p0, c0), u1 = mul_conj(p1, c1);
+    // 1 / (|u| 2^-32) = rsq(|c|^2 |p|^2 2^-64), then the 2^-32 back
+    const c2 q = (mk(cn0, cn1) * mk(0x1p-64f, 0x1p-64f)) * mk(pn0, pn1);
+    const c2 r = mk(__builtin_amdgcn_rsqf(fmaxf(q.x, 0x1p-126f)), __builtin_amdgcn_rsqf(fmaxf(q.y, 0x1p-126f))) *
+                 mk(0x1p-32f, 0x1p-32f);
+    c2 x = mk(u0.x, u1.x) * r, y = mk(u0.y, u1.y) * (r * mk(sp.S_sgn, sp.S_sgn));
+    cpow_x2<E>(x, y);
+    v0 = mul(c0, mk(mmag0 * x.x + mpass0, mmag0 * y.x));
+    v1 = mul(c1, mk(mmag1 * x.y + mpass1, mmag1 * y.y));
+    p0 = c0;
+    p1 = c1;
+}
+
+// one bin (the packed group's one-at-a-time ops): the two-bin form with the
+// second lane a copy
+template <int E, bool TWO>
+__device__ __forceinline__ c2 pyramid_op_pow1(c2 c, c2 p, const Spec &sp, float2 mt, float ms)
+{
+    c2 v0 = c, p0 = p, v1 = c, p1 = p;
+    pyramid_op_pow_x2<E, TWO>(v0, p0, mt, ms, v1, p1, mt, ms, sp);
+    return v0;
+}
 template <int MODE>
 __device__ __forceinline__ c2 standard_op_t(c2 c, c2 p, const Spec &sp, float2 mt)
 {
@@ -980,7 +992,21 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
 
 // k_cols runs at least two columns per workgroup, so that a Q row receives one
 // 16-B (or wider) piece per workgroup instead of one 8-B value per column
-template <int LOG2N> constexpr int k2_groups() { return groups_at_least<LOG2N, MM_K2_GROUPS>(); }
+// two columns per k_cols workgroup (whole 32-B Q pieces per tile row) up to
+// N = 2048; at N = 4096 a two-column workgroup is 16 waves with 123-148 KB of
+// LDS, one per CU for the whole launch (every s_barrier stalls the whole
+// CU), so there k_cols runs one column per workgroup (8 waves, <= 62 KB
+// without the packed group's arrays: two per CU; MM_K2_GROUPS_4K)
+#ifndef MM_K2_GROUPS_4K
+#define MM_K2_GROUPS_4K 1
+#endif
+template <int LOG2N> constexpr int k2_groups()
+{
+    return LOG2N >= 12 ? MM_K2_GROUPS_4K : groups_at_least<LOG2N, MM_K2_GROUPS>();
+}
+// the steerable band-column kernel: two columns per workgroup at every N
+template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, 2>(); }
+template <int LOG2N> constexpr int sb_threads() { return sb_groups<LOG2N>() * fft_T<LOG2N>(); }
 // K2's Q staging buffer (c2 slots written by rows, read back as float4
 // pieces): slot i lives at i ^ (((i >> 4) & 1) << 1), i.e. float4 r at
 // r ^ ((r >> 3) & 1).  The row writes of a 16-lane group (every other float4
@@ -1011,27 +1037,31 @@ template <int LOG2N> constexpr bool k2_twtab() { return MM_K2_TWTAB && fft_c_v(L
 // workgroup's GPW columns, [Hq/TK][GPW][TK] c2 (k2_stg_swz stays inside
 // 32-slot blocks), when it fits beside two workgroups per CU (1080p: 17 KB);
 // else 0 (aliased with the exchange buffers).
-template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes();
-template <int LOG2N, int MODE> inline int k2_stg_c2(int Hq)
+template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes(bool with_packed = true);
+template <int LOG2N, int MODE> inline int k2_stg_c2(int Hq, bool with_packed = true)
 {
     const int c = (Hq * k2_groups<LOG2N>() + 31) / 32 * 32;
-    return k2_lds_bytes<LOG2N, MODE>() + sizeof(c2) * (size_t)c <= 81920 ? c : 0;
+    return k2_lds_bytes<LOG2N, MODE>(with_packed) + sizeof(c2) * (size_t)c <= 81920 ? c : 0;
 }
 
-// bytes of the mask-sum arrays (pyramid tables: GPW + 1 columns' [TS] floats,
-// rounded up to 16 B)
-template <int LOG2N, int MODE> constexpr size_t k2_msum_bytes()
+// bytes of n columns' mask-sum arrays ([TS] floats each, rounded up to 16 B;
+// pyramid tables with overlapping bands only)
+template <int LOG2N, int MODE> constexpr size_t k2_msum_bytes(int n)
 {
-    return k2_msum<MODE>()
-               ? ((sizeof(float) * (size_t)(k2_groups<LOG2N>() + 1) * k2_tab_slots<LOG2N>()) + 15) / 16 * 16
-               : 0;
+    return k2_msum<MODE>() ? ((sizeof(float) * (size_t)n * k2_tab_slots<LOG2N>()) + 15) / 16 * 16 : 0;
 }
-template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes()
+// k_cols' dynamic LDS, in layout order: the GPW exchange buffers, the GPW
+// columns' tables and mask sums, the inner twiddle table (TT); then what only
+// the packed group (block 0) uses: column N/2's table and mask sums and ldsX.
+// A launch without block 0 (its frames all in k_cols_tail) omits that last part.
+template <int LOG2N, int MODE> constexpr size_t k2_lds_bytes(bool with_packed)
 {
     return (size_t)k2_groups<LOG2N>() *
                (sizeof(c2) * lds_complex<(1 << LOG2N)>() + sizeof(float2) * k2_tab_slots<LOG2N>()) +
-           sizeof(float2) * k2_tab_slots<LOG2N>() + k2_msum_bytes<LOG2N, MODE>() + sizeof(c2) * 4 +
-           (k2_twtab<LOG2N>() ? sizeof(float4) * tw_tab_float4() : 0);
+           k2_msum_bytes<LOG2N, MODE>(k2_groups<LOG2N>()) +
+           (k2_twtab<LOG2N>() ? sizeof(float4) * tw_tab_float4() : 0) +
+           (with_packed ? sizeof(float2) * k2_tab_slots<LOG2N>() + k2_msum_bytes<LOG2N, MODE>(1) + sizeof(c2) * 4
+                        : 0);
 }
 
 // Columns f = 1..N/2-1 get one FFT group each.  The two real columns f = 0 and
@@ -1075,7 +1105,7 @@ __device__ unsigned long long mm_k2_exit[4096 * 8];    // ... after the last Q s
 // the forward transform as a passthrough frame (fr = -1), which sets F_{t-1}
 // in registers bit for bit as the frame loop would have, then frames
 // 0 .. nframes-1 of G, whose Q go to Q + fr * q_stride.
-template <int LOG2N, int MODE, bool BLK0>
+template <int LOG2N, int MODE, bool BLK0, int SP = 0>
 __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q,
                                             size_t q_stride, int nframes, const Geo &g,
                                             const Spec &sp, const c2 *__restrict__ tw,
@@ -1097,16 +1127,21 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     // exchange buffers (two more workgroup barriers per frame)
     c2 *xbase = lds_all + stg_c2;
     c2 *lds = xbase + grp * lds_complex<N>();
-    float2 *tab0 = reinterpret_cast<float2 *>(xbase + GPW * lds_complex<N>()) + grp * TS;
-    float2 *tabN = reinterpret_cast<float2 *>(xbase + GPW * lds_complex<N>()) + GPW * TS;
+    float2 *tabs = reinterpret_cast<float2 *>(xbase + GPW * lds_complex<N>());
+    float2 *tab0 = tabs + grp * TS;
     // column N/2: F_{t-1} at its real bins 0 and N/2 and their results (two
     // threads of the packed group).  Its Q values are staged with column 0's:
     // the packed group's staging slot of a row holds (Q0, QN) (the inverse of
     // A0 + i AN; both real), split into the two columns' pieces at the store.
     // the bins' whole mask sums (tabled pyramid modes; two-band waves read them)
-    float *ms0 = reinterpret_cast<float *>(tabN + TS) + grp * TS;
-    float *msN = reinterpret_cast<float *>(tabN + TS) + GPW * TS;
-    c2 *ldsX = reinterpret_cast<c2 *>(reinterpret_cast<uint8_t *>(tabN + TS) + k2_msum_bytes<LOG2N, MODE>());
+    float *ms0 = reinterpret_cast<float *>(tabs + GPW * TS) + grp * TS;
+    uint8_t *lds_tail = reinterpret_cast<uint8_t *>(tabs + GPW * TS) + k2_msum_bytes<LOG2N, MODE>(GPW);
+    float4 *ttab = reinterpret_cast<float4 *>(lds_tail);   // inner passes' twiddle powers (TT)
+    if constexpr (k2_twtab<LOG2N>()) lds_tail += sizeof(float4) * tw_tab_float4();
+    // packed group only (k2_lds_bytes with_packed): column N/2's table, mask sums, ldsX
+    float2 *tabN = reinterpret_cast<float2 *>(lds_tail);
+    float *msN = reinterpret_cast<float *>(tabN + TS);
+    c2 *ldsX = reinterpret_cast<c2 *>(reinterpret_cast<uint8_t *>(msN) + k2_msum_bytes<LOG2N, MODE>(1));
     const int f_raw = blk * GPW + grp;
     const bool valid = f_raw < N / 2;
     const int f = valid ? f_raw : N / 2 - 1;
@@ -1154,7 +1189,6 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #endif
     // twiddle bases of both FFTs, loaded once (issued under the table copy): no loads inside a frame but G's
     constexpr bool TT = k2_twtab<LOG2N>();
-    float4 *ttab = reinterpret_cast<float4 *>(ldsX + 4);   // inner passes' twiddle powers (TT)
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
@@ -1350,27 +1384,6 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             if (pass_frame) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) prev[j] = v[j];
-            } else if (MODE == MM_K2_PYR_POW && !wave_two_band) {
-                // integer phase scale: the power form, two bins at a time (the
-                // table addressing of the branch above)
-                constexpr int C = fft_c_v(LOG2N);
-                const int fy0 = fft_bin<LOG2N>(HOIST ? t0 : t, 0);   // frame-invariant (hoisted: t0)
-                const int w = fy0 % C;
-                const float2 *tlo = HOIST ? tlo0 : tab0 + k2_tix<LOG2N>(fy0);
-                const float2 *thi = HOIST ? thi0 : tab0 + (w ? k2_tix<LOG2N>(C - w) - 1 : 0) - fy0 / C;
-#ifndef MM_K2_POWG
-#define MM_K2_POWG 4   // bins per power loop (its scalar control and phi moves amortise over them; 8 spills)
-#endif
-#pragma unroll
-                for (int j = 0; j < 8; j += MM_K2_POWG) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    float2 mt[MM_K2_POWG];
-#pragma unroll
-                    for (int b = 0; b < MM_K2_POWG; ++b)
-                        mt[b] = j + b < 4 ? tlo[(j + b) * (N / 8) / C] : thi[(N - (j + b) * (N / 8)) / C];
-                    pyramid_op_pow<MM_K2_POWG>(v, prev, j, mt, sp);
-                }
-                __builtin_amdgcn_sched_barrier(0);
             } else if (k2_one_band_op<MODE>() && !wave_two_band) {
                 // no bin of this wave has two middle bands: branch-free op, bins
                 // interleaved MM_K2_OPG at a time
@@ -1394,7 +1407,10 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     if (j % MM_K2_OPX2G == 0) __builtin_amdgcn_sched_barrier(0);
                     const float2 mt0 = j < 4 ? tlo[j * (N / 8) / C] : thi[(N - j * (N / 8)) / C];
                     const float2 mt1 = j + 1 < 4 ? tlo[(j + 1) * (N / 8) / C] : thi[(N - (j + 1) * (N / 8)) / C];
-                    pyramid_op_1band_x2(v[j], prev[j], mt0, v[j + 1], prev[j + 1], mt1, sp);
+                    if constexpr (SP > 0)
+                        pyramid_op_pow_x2<SP, false>(v[j], prev[j], mt0, 0.0f, v[j + 1], prev[j + 1], mt1, 0.0f, sp);
+                    else
+                        pyramid_op_1band_x2(v[j], prev[j], mt0, v[j + 1], prev[j + 1], mt1, sp);
                 }
 #else
 #pragma unroll
@@ -1423,7 +1439,10 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     const int i1 = j + 1 < 4 ? (j + 1) * (N / 8) / C : (N - (j + 1) * (N / 8)) / C;
                     const float2 mt0 = j < 4 ? tlo[i0] : thi[i0], mt1 = j + 1 < 4 ? tlo[i1] : thi[i1];
                     const float s0 = j < 4 ? mlo[i0] : mhi[i0], s1 = j + 1 < 4 ? mlo[i1] : mhi[i1];
-                    pyramid_op_2band_x2(v[j], prev[j], mt0, s0, v[j + 1], prev[j + 1], mt1, s1, sp);
+                    if constexpr (SP > 0)
+                        pyramid_op_pow_x2<SP, true>(v[j], prev[j], mt0, s0, v[j + 1], prev[j + 1], mt1, s1, sp);
+                    else
+                        pyramid_op_2band_x2(v[j], prev[j], mt0, s0, v[j + 1], prev[j + 1], mt1, s1, sp);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             } else {
@@ -1459,23 +1478,17 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     v[j] = pk_col0(j, fy) ? f0 : mk(fn.x, -fn.y);                // or FN(N - fy)
                 }
                 if (!pass_frame) {
-                    if (MODE == MM_K2_PYR_POW && !wave_two_band) {
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
-                            const int fy = fft_bin<LOG2N>(t, j);
-                            const float2 mt[1] = {pk_col0(j, fy) ? tab0[k2_tix<LOG2N>(fy)]
-                                                                 : tabN[k2_tix<LOG2N>(N - fy)]};
-                            pyramid_op_pow<1>(v, prev, j, mt, sp);
-                        }
-                    } else if (k2_one_band_op<MODE>() && !wave_two_band) {
+                    if (k2_one_band_op<MODE>() && !wave_two_band) {
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             __builtin_amdgcn_sched_barrier(0);   // one bin at a time: registers
                             const int fy = fft_bin<LOG2N>(t, j);
                             const c2 c = v[j];
-                            v[j] = pyramid_op_1band(c, prev[j], sp, pk_col0(j, fy) ? tab0[k2_tix<LOG2N>(fy)]
-                                                                                   : tabN[k2_tix<LOG2N>(N - fy)]);
+                            const float2 mt = pk_col0(j, fy) ? tab0[k2_tix<LOG2N>(fy)] : tabN[k2_tix<LOG2N>(N - fy)];
+                            if constexpr (SP > 0)
+                                v[j] = pyramid_op_pow1<SP, false>(c, prev[j], sp, mt, 0.0f);
+                            else
+                                v[j] = pyramid_op_1band(c, prev[j], sp, mt);
                             prev[j] = c;
                         }
                     } else if (MODE == MM_K2_PYR_TAB2) {   // two-band waves
@@ -1486,7 +1499,12 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                             const bool c0 = pk_col0(j, fy);
                             const int ix = k2_tix<LOG2N>(c0 ? fy : N - fy);
                             const c2 c = v[j];
-                            v[j] = pyramid_op_2band(c, prev[j], sp, c0 ? tab0[ix] : tabN[ix], c0 ? ms0[ix] : msN[ix]);
+                            if constexpr (SP > 0)
+                                v[j] = pyramid_op_pow1<SP, true>(c, prev[j], sp, c0 ? tab0[ix] : tabN[ix],
+                                                                 c0 ? ms0[ix] : msN[ix]);
+                            else
+                                v[j] = pyramid_op_2band(c, prev[j], sp, c0 ? tab0[ix] : tabN[ix],
+                                                        c0 ? ms0[ix] : msN[ix]);
                             prev[j] = c;
                         }
                     } else {
@@ -1624,11 +1642,12 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #define MM_K2_WAVES 4
 #endif
 
-template <int LOG2N, int MODE>
+template <int LOG2N, int MODE, int SP = 0>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
 void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride,   // not restrict: G loads must stay ahead of Q stores
             int nframes, Geo g, Spec sp, const c2 *__restrict__ tw, const float2 *__restrict__ ktab,
-            const float *__restrict__ kmsum, int stg_c2, int nframes_blk0, int tail_blocks, int ktail)
+            const float *__restrict__ kmsum, int stg_c2, int nframes_blk0, int tail_blocks, int ktail,
+            int pk_off)
 {
     // Blocks nb .. nb + tail_blocks - 1 (tail_blocks <= nb / 2) are tails: the
     // last ktail frames of the columns of second-half block nb/2 + i, which
@@ -1637,19 +1656,21 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
     // (phase stamps: first half done at ~825 us, second at ~1,045 us per 100
     // frames); its tail starts in the slot the first one frees, primed with the
     // frame before its first (the state is a pure function of that frame).
+    // pk_off = 1: block 0 (the packed group) is not in this launch (all its
+    // frames run in k_cols_tail): the column blocks are 1 .. nb
     const int nb = gridDim.x - tail_blocks;
     const bool tail = (int)blockIdx.x >= nb;
     const int p = tail ? nb / 2 + ((int)blockIdx.x - nb) : (int)blockIdx.x;
     // same-XCD blocks own consecutive columns, so the pieces of one 128-B Q line
     // are merged in one L2 (split over XCDs they left as partial-line writes)
-    const int blk = xcd_remap(p, nb);
+    const int blk = xcd_remap(p, nb) + pk_off;
     if (blk == 0) {   // the packed block stops nframes_blk0 frames in (k_cols_tail)
-        k_cols_body<LOG2N, MODE, true>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, kmsum, stg_c2,
+        k_cols_body<LOG2N, MODE, true, SP>(G, g_stride, Gprev, Q, q_stride, nframes_blk0, g, sp, tw, ktab, kmsum, stg_c2,
                                        blk, nb);
     } else {
         const int f0 = tail ? nframes - ktail : 0;
         const int nf = tail ? ktail : (p >= nb / 2 && p - nb / 2 < tail_blocks ? nframes - ktail : nframes);
-        k_cols_body<LOG2N, MODE, false>(G + (size_t)f0 * g_stride, g_stride,
+        k_cols_body<LOG2N, MODE, false, SP>(G + (size_t)f0 * g_stride, g_stride,
                                         tail ? G + (size_t)(f0 - 1) * g_stride : Gprev,
                                         Q + (size_t)f0 * q_stride, q_stride, nf, g, sp, tw, ktab, kmsum, stg_c2,
                                         blk, nb);
@@ -1665,15 +1686,16 @@ void k_cols(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_strid
 // function of the previous input frame (.cs:142), so workgroup i primes with
 // frame f0 + i - 1 (its passthrough frame sets F_{t-1} exactly as the frame
 // loop would: bitwise the same outputs) and then runs frame f0 + i.
-template <int LOG2N, int MODE>
+template <int LOG2N, int MODE, int SP = 0>
 __global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(MM_K2_WAVES)))
-void k_cols_tail(const c2 *G, size_t g_stride, c2 *Q, size_t q_stride, int f0, Geo g, Spec sp,
+void k_cols_tail(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q, size_t q_stride, int f0, Geo g, Spec sp,
                  const c2 *__restrict__ tw, const float2 *__restrict__ ktab, const float *__restrict__ kmsum,
                  int stg_c2)
 {
-    const int fr = f0 + (int)blockIdx.x;   // >= 1
-    k_cols_body<LOG2N, MODE, true>(G + (size_t)fr * g_stride, g_stride, G + (size_t)(fr - 1) * g_stride,
-                                   Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, kmsum, stg_c2, 0);
+    const int fr = f0 + (int)blockIdx.x;   // frame 0 primes with the state slot
+    k_cols_body<LOG2N, MODE, true, SP>(G + (size_t)fr * g_stride, g_stride,
+                                       fr > 0 ? G + (size_t)(fr - 1) * g_stride : Gprev,
+                                       Q + (size_t)fr * q_stride, q_stride, 1, g, sp, tw, ktab, kmsum, stg_c2, 0);
 }
 
 // K2's per-bin tables of every column in LDS slot order ([N/2+1][k2_tab_slots]):

@@ -101,11 +101,11 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
 // band loop issues no loads (twiddle bases hoisted), so its stores are never
 // waited for.
 template <int LOG2N>
-__global__ __launch_bounds__(k2_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(sb_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_stride, Geo g, Spec sp,
                const c2 *__restrict__ tw)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = k2_groups<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = sb_groups<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
     const int t0 = threadIdx.x % T;

@@ -500,3 +500,23 @@ def test_two_band_op_tail_and_batch_bitwise(monkeypatch):
     c = T.gpu_run(W, H, fr, 6, 25.0, mode="frame", batch=1)
     for x, y, z in zip(a, b, c):
         assert np.array_equal(x, y) and np.array_equal(x, z)
+
+
+# ---- round 4: the packed block entirely in k_cols_tail (MM_K2_PKALL) --------------
+@pytest.mark.parametrize("W,H,L,n,batch", [(1920, 1080, 5, 30, 30), (1920, 1080, 6, 30, 30),
+                                           (640, 360, 5, 60, 25), (2100, 64, 6, 50, 25)])
+def test_k2_packed_all_in_tail_bitwise(W, H, L, n, batch, monkeypatch):
+    """Batches >= 24 frames with block 0 (the packed group) out of k_cols and
+    every one of its frames a k_cols_tail workgroup (frame 0 primed from the
+    state slot, the others from the previous input frame): bitwise the
+    outputs with block 0 in k_cols and of one-frame calls.  2100 x 64 is
+    N = 4096, where it is the default (one-column workgroups, two per CU)."""
+    fr = T.synth(W, H, n, fmt="u8")
+    monkeypatch.setenv("MM_K2_PKALL", "0")
+    a = T.gpu_run(W, H, fr, L, 25.0, mode="stream", batch=batch)
+    monkeypatch.setenv("MM_K2_PKALL", "1")
+    b = T.gpu_run(W, H, fr, L, 25.0, mode="stream", batch=batch)
+    monkeypatch.delenv("MM_K2_PKALL")
+    c = T.gpu_run(W, H, fr, L, 25.0, mode="frame", batch=1)
+    for x, y, z in zip(a, b, c):
+        assert np.array_equal(x, y) and np.array_equal(x, z)
