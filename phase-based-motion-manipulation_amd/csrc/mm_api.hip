@@ -318,13 +318,13 @@ static bool bands_overlap(const Spec &sp)
     return false;
 }
 
-// k_cols' power-form instance for this handle (mm_kernels.hpp cpow_x2): |S|
-// for an integer phase scale with a compiled instance (|S| 25 and 10, the
-// configurations' values, at N >= 2048), else 0 (the atan2 form).
-// MM_K2_POW=0 selects the atan2 form throughout.
+// k_cols' power-form instance for this handle (mm_kernels.hpp cpow_x2), opt-in
+// with MM_K2_POW=1 (measured slower than the atan2 form): |S| for an integer
+// phase scale with a compiled instance (|S| 25 and 10, the configurations'
+// values, at N >= 2048), else 0 (the atan2 form).
 static int k2_power_exponent(const Spec &sp, int N)
 {
-    if (getenv("MM_K2_POW") && atoi(getenv("MM_K2_POW")) == 0) return 0;
+    if (!getenv("MM_K2_POW") || atoi(getenv("MM_K2_POW")) == 0) return 0;
     return N >= 2048 && (sp.S_pow == 25 || sp.S_pow == 10) ? sp.S_pow : 0;
 }
 
@@ -569,10 +569,18 @@ static bool k34_fits(const mm_handle *h)
 // pair (0) when that would take strips under 16 rows (the one-frame drop-in
 // call: K3 + K4 spread one frame over thousands of workgroups).  MM_K34_ROWS
 // forces a strip height (0: unfused).
+#ifndef MM_K34_ROWS_4K
+#define MM_K34_ROWS_4K 128
+#endif
 static int k34_strip_rows(const mm_handle *h, int nout)
 {
     if (h->k34_rows >= 0) return h->k34_rows;
-    const int R = std::min(64, (int)((long long)h->H * nout / 1024) / 4 * 4);
+    // at N = 4096 a K34 workgroup (1,024 threads, 125 VGPRs) is alone on its
+    // CU, so a longer strip halves the halo rows at no cost in concurrency
+    // (C3 same-call: R 64 -> 128, K34 26.4-26.8 -> 25.7-25.8 us per frame;
+    // at 1080p 96 and 128 were slower than 64)
+    const int cap = h->N >= 4096 ? MM_K34_ROWS_4K : 64;
+    const int R = std::min(cap, (int)((long long)h->H * nout / 1024) / 4 * 4);
     return R >= 16 ? R : 0;
 }
 
@@ -1189,9 +1197,11 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->ktab_mode = -1;
     h->blur = build_blur();
     h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
-    // N = 4096 (one-column workgroups, k2_groups): k_cols fits two workgroups
-    // per CU only without the packed group's LDS arrays (MM_K2_PKALL 0 / 1)
-    h->k2_pk_all = getenv("MM_K2_PKALL") ? atoi(getenv("MM_K2_PKALL")) != 0 : N >= 4096;
+    // every packed-block frame in k_cols_tail (MM_K2_PKALL=1): what lets a
+    // one-column N = 4096 build (-DMM_K2_GROUPS_4K=1) fit two workgroups per
+    // CU; same-call no faster at the default shapes (1080p 8.54 vs 8.58 us,
+    // C3 within noise), so off by default
+    h->k2_pk_all = getenv("MM_K2_PKALL") && atoi(getenv("MM_K2_PKALL")) != 0;
     // dedicated Q staging: 2 barriers per frame fewer, but same-call K2 +1 %
     // at 1080p (r04d); opt-in (MM_K2_STGD=1)
     h->k2_stg_ded = getenv("MM_K2_STGD") && atoi(getenv("MM_K2_STGD")) == 1;

@@ -882,7 +882,11 @@ __device__ __forceinline__ c2 pyramid_op_2band(c2 c, c2 p, const Spec &sp, float
 // squarings and products, two bins per packed op: |S| = 25 is 4 squarings + 2
 // products, 10 is 3 + 1.  S < 0: conj(z)^|S| (the sign on z's imaginary part).
 // Same value up to fp32 rounding (tests/test_k2_pow.py against the atan2 form
-// and the oracle).  Range: |p| |c| < 2^64 (the product of the squared norms is
+// and the oracle).  Opt-in (MM_K2_POW=1): it trades the atan2 polynomial and
+// 3 transcendentals per bin for 1 rsq and 12 packed ops per bin (|S| = 25),
+// +15 VALU per 8 bins at 16 fewer transcendental issue slots, and measured
+// slower same-call (1080p k_cols 8.38 -> 8.58-8.61 us, C3 38.6-39.0 ->
+// 39.1-39.4: the squaring chain is one long dependency per bin pair).  Range: |p| |c| < 2^64 (the product of the squared norms is
 // scaled by 2^-64 before the rsq; any RGBA8 frame is below 2^25 per bin), and
 // a bin with |p|^2 |c|^2 < 2^-62 gets z = u 2^31 instead of u / |u| (such a bin
 // is gated unless tau < 2^-31 / (m N M)).
@@ -992,13 +996,14 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
 
 // k_cols runs at least two columns per workgroup, so that a Q row receives one
 // 16-B (or wider) piece per workgroup instead of one 8-B value per column
-// two columns per k_cols workgroup (whole 32-B Q pieces per tile row) up to
-// N = 2048; at N = 4096 a two-column workgroup is 16 waves with 123-148 KB of
-// LDS, one per CU for the whole launch (every s_barrier stalls the whole
-// CU), so there k_cols runs one column per workgroup (8 waves, <= 62 KB
-// without the packed group's arrays: two per CU; MM_K2_GROUPS_4K)
+// two columns per k_cols workgroup (whole 32-B Q pieces per tile row).  At
+// N = 4096 that is 16 waves with 123-148 KB of LDS, one workgroup per CU for
+// the whole launch; one column per workgroup there (8 waves, <= 62 KB without
+// the packed group's arrays, MM_K2_PKALL: two per CU) measured slower
+// same-call (C3 k_cols 37.5 -> 38.6-39.0 us per frame: 16-B Q pieces), so it
+// is a build option only (-DMM_K2_GROUPS_4K=1).
 #ifndef MM_K2_GROUPS_4K
-#define MM_K2_GROUPS_4K 1
+#define MM_K2_GROUPS_4K 2
 #endif
 template <int LOG2N> constexpr int k2_groups()
 {

@@ -509,8 +509,8 @@ def test_k2_packed_all_in_tail_bitwise(W, H, L, n, batch, monkeypatch):
     """Batches >= 24 frames with block 0 (the packed group) out of k_cols and
     every one of its frames a k_cols_tail workgroup (frame 0 primed from the
     state slot, the others from the previous input frame): bitwise the
-    outputs with block 0 in k_cols and of one-frame calls.  2100 x 64 is
-    N = 4096, where it is the default (one-column workgroups, two per CU)."""
+    outputs with block 0 in k_cols and of one-frame calls (2100 x 64: N =
+    4096).  Opt-in (MM_K2_PKALL=1): same-call no faster at the default shapes."""
     fr = T.synth(W, H, n, fmt="u8")
     monkeypatch.setenv("MM_K2_PKALL", "0")
     a = T.gpu_run(W, H, fr, L, 25.0, mode="stream", batch=batch)

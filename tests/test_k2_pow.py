@@ -1,9 +1,10 @@
 """K2's power form of the phase factor (k_cols SP > 0: an integer phase scale
-with a compiled instance, |S| 25 and 10 at N >= 2048, the default there):
+with a compiled instance, |S| 25 and 10 at N >= 2048; opt-in, MM_K2_POW=1,
+measured slower than the atan2 form):
 e^{i S wrap(arg p - arg c)} = z^S with z = p conj(c) / |p||c|
 (PyramidPhaseDifference.compute:47-54, 92-98: for integer S the wrap's
 multiple of 2 pi drops out).  Against the atan2 + sin/cos form of the same
-kernel (MM_K2_POW=0) and against the oracle's literal atan2f path: one-band
+kernel (the default) and against the oracle's literal atan2f path: one-band
 (L = 5) and two-band (L = 6) layouts, S < 0, the stream's batch, tail and
 packed-group paths, and the 1080p RGBA8 bench geometry."""
 import os
@@ -17,10 +18,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(W, H, fr, S, atan2_form, L=5, mode="stream", batch=3):
-    """atan2_form: MM_K2_POW=0 (read at mm_create); else the default."""
+    """atan2_form: the default; else MM_K2_POW=1 (read at mm_create)."""
     old = os.environ.pop("MM_K2_POW", None)
-    if atan2_form:
-        os.environ["MM_K2_POW"] = "0"
+    if not atan2_form:
+        os.environ["MM_K2_POW"] = "1"
     try:
         return T.gpu_run(W, H, fr, L, S, mode=mode, batch=batch)
     finally:
@@ -46,7 +47,7 @@ def test_power_form_matches_atan2_form_and_oracle(S, L):
 
 @pytest.mark.parametrize("S", [7.0, 25.5])
 def test_other_scales_keep_the_atan2_form(S):
-    """No compiled instance (|S| = 7) or a non-integer S: MM_K2_POW has no effect."""
+    """No compiled instance (|S| = 7) or a non-integer S: MM_K2_POW=1 has no effect."""
     W, H = 1100, 48
     fr = T.synth(W, H, 3)
     assert all(np.array_equal(a, b) for a, b in zip(_run(W, H, fr, S, False), _run(W, H, fr, S, True)))

@@ -129,7 +129,8 @@ def test_oneshot_standard_mode_and_oracle():
 
 @pytest.mark.parametrize("W,H,rows,edge,fmt", [
     (200, 120, 64, 0, "f32"), (200, 120, 8, 1, "f32"), (200, 118, 4, 0, "u8"),
-    (240, 136, 12, 1, "u8"), (120, 200, 32, 0, "f32"), (504, 250, 16, 1, "u8")])
+    (240, 136, 12, 1, "u8"), (120, 200, 32, 0, "f32"), (504, 250, 16, 1, "u8"),
+    (2100, 300, 128, 0, "u8"), (2100, 300, 256, 1, "f32")])
 def test_fused_equals_unfused_bitwise(W, H, rows, edge, fmt):
     fr = T.synth(W, H, 5, fmt=fmt)
     a = _run_env(rows, W, H, fr, 5, 25.0, edge, mode="stream")
@@ -173,7 +174,8 @@ def test_fused_equals_unfused_2160p_u8():
     of dynamic LDS (hipFuncSetAttribute at mm_create)."""
     W, H = 3840, 2160
     fr = T.synth(W, H, 3, fmt="u8")
-    a = _run_env(64, W, H, fr, 6, 25.0, 0, mode="stream")
     b = _run_env(0, W, H, fr, 6, 25.0, 0, mode="stream")
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
+    for rows in (64, 128):   # 128: the N = 4096 default strip (MM_K34_ROWS_4K)
+        a = _run_env(rows, W, H, fr, 6, 25.0, 0, mode="stream")
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
