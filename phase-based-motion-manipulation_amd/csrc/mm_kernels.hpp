@@ -1298,7 +1298,16 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
     st_acc[7] = __builtin_amdgcn_s_memrealtime();   // loop start (100 MHz, device-wide)
 #endif
-    for (int fr = -1;; ++fr) {
+    // One frame of the loop.  The prime (fr = -1) runs as its own instance
+    // ahead of the loop, so the frame loop itself is compiled with no
+    // passthrough branch: in one shared body the branch merge made the
+    // compiler copy the FFT outputs twice per frame (once for the merge, once
+    // into the loop-carried F_{t-1}: 32 v_mov; K2 -2 % at 1080p, -3 % at
+    // 2160p same-call).  The prime keeps a RUNTIME passthrough test (fr is
+    // made opaque): an instance specialised on a constant fr = -1 computed an
+    // F_{t-1} 1 ulp away from the in-loop one, which broke the bitwise
+    // equality of one-frame calls, tails, ring hand-offs and batches.
+    auto frame_iter = [&](const int fr) __attribute__((always_inline)) -> bool {
         // Opaque per-iteration copy of the lane index: stops LICM from hoisting
         // every t-derived LDS address and twiddle of both FFTs out of the frame
         // loop (that pinned ~200 VGPRs and capped occupancy at 1 wave/SIMD).
@@ -1365,7 +1374,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             }
         }
         K2_STAMP(1);
-        if (fr == nframes) break;
+        if (fr == nframes) return false;
         c2 v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j)   // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
@@ -1383,7 +1392,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         fft_dif<LOG2N, -1, TT>(v, t, lds, wt, ttab);
         MM_MARK("M2_fwd_end");
         K2_STAMP(3);
-        const bool pass_frame = fr < 0;
+        const bool pass_frame = fr < 0;   // the prime (fr = -1)
         // the spectral op of a regular group (all groups but the packed one)
         auto regular_op = [&]() {
             if (pass_frame) {
@@ -1627,7 +1636,15 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         }   // !pass_frame
         __syncthreads();   // staged pieces complete (stored at the top of the next iteration)
         K2_STAMP(6);
+        return true;
+    };
+    {
+        int fr_prime = -1;   // opaque: the prime instance keeps the runtime passthrough test
+        asm volatile("" : "+s"(fr_prime));
+        frame_iter(fr_prime);
     }
+    for (int fr = 0;; ++fr)
+        if (!frame_iter(fr)) break;   // (fr >= 0 here: no passthrough branch)
 #ifdef MM_K2_STAMPS
     st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
     __builtin_amdgcn_s_waitcnt(0);   // every load and store of the wave completed
