@@ -527,6 +527,33 @@ __device__ __forceinline__ float fast_atan2(float y, float x)
     return copysignf(r, y);
 }
 
+// fast_atan2 of two arguments at once: the polynomial, its reconstruction
+// constant and the scale run as packed FP32 (v_pk_fma_f32: a fused
+// multiply-add per half, so both results are fast_atan2's bit for bit); the
+// octant selects stay scalar (VOP3P has no abs modifier)
+__device__ __forceinline__ c2 fast_atan2_x2(float y0, float x0, float y1, float x1)
+{
+    const float ax0 = fabsf(x0), ay0 = fabsf(y0), ax1 = fabsf(x1), ay1 = fabsf(y1);
+    const bool st0 = ay0 > ax0, st1 = ay1 > ax1;
+    const float a0 = (st0 ? ax0 : ay0) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(ax0, ay0), 1.17549435e-38f));
+    const float a1 = (st1 ? ax1 : ay1) * __builtin_amdgcn_rcpf(fmaxf(fmaxf(ax1, ay1), 1.17549435e-38f));
+    const c2 a = mk(a0, a1), sq = a * a;
+    c2 r = mk(-0.00405455008149147f, -0.00405455008149147f);
+    r = r * sq + mk(0.021862903609871864f, 0.021862903609871864f);
+    r = r * sq - mk(0.055912263691425323f, 0.055912263691425323f);
+    r = r * sq + mk(0.09642193466424942f, 0.09642193466424942f);
+    r = r * sq - mk(0.1390862911939621f, 0.1390862911939621f);
+    r = r * sq + mk(0.19946566224098206f, 0.19946566224098206f);
+    r = r * sq - mk(0.33329859375953674f, 0.33329859375953674f);
+    r = r * sq + mk(0.9999993443489075f, 0.9999993443489075f);
+    const c2 ra = r * a;
+    const c2 rs = mk(1.57079632679489662f, 1.57079632679489662f) - ra;
+    float t0 = st0 ? rs.x : ra.x, t1 = st1 ? rs.y : ra.y;
+    if (x0 < 0.0f) t0 = 3.14159265358979324f - t0;
+    if (x1 < 0.0f) t1 = 3.14159265358979324f - t1;
+    return mk(copysignf(t0, y0), copysignf(t1, y1));
+}
+
 // Radial masks of GeneratePyramidFilters (PyramidOperations.compute:25-87) and the
 // per-level gate/phase rule of ProcessPyramidPhaseDifference
 // (PyramidPhaseDifference.compute:58-101), summed over levels

@@ -302,9 +302,17 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
         }
         // this band's new state and amplified synthesis, in registers
         float nph[8], nuh[8], nul[8];
+        // local phases two bins at a time (packed FP32, fast_atan2's values)
+        float phs[8];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            const c2 p2 = fast_atan2_x2(v[j].y, v[j].x, v[j + 1].y, v[j + 1].x);
+            phs[j] = p2.x;
+            phs[j + 1] = p2.y;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float ph = fast_atan2(v[j].y, v[j].x);
+            const float ph = phs[j];
             float P = 0.0f, uh = 0.0f, ul = 0.0f;
             if (!reset) {
                 if (!iir) {
