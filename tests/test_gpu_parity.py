@@ -520,3 +520,22 @@ def test_k2_packed_all_in_tail_bitwise(W, H, L, n, batch, monkeypatch):
     c = T.gpu_run(W, H, fr, L, 25.0, mode="frame", batch=1)
     for x, y, z in zip(a, b, c):
         assert np.array_equal(x, y) and np.array_equal(x, z)
+
+
+# ---- K2's generic per-bin op (MM_MODE_PYRAMID instance) ---------------------------
+@pytest.mark.parametrize("W,H,L,S,notab", [(200, 120, 7, 25.0, False), (160, 96, 8, 9.7, False),
+                                           (200, 120, 5, 25.0, True)])
+def test_k2_generic_op_vs_oracle(W, H, L, S, notab, monkeypatch):
+    """Band layouts where three middle bands share bins (L >= 7 at the default
+    0.05 / 0.45) and MM_K2_NOTAB=1 run K2's generic per-bin op: against the
+    oracle in a stream and in one-frame calls, which agree bitwise."""
+    if notab:
+        monkeypatch.setenv("MM_K2_NOTAB", "1")
+    fr = T.synth(W, H, 5)
+    ref = T.oracle_run(W, H, fr, L, S)
+    st = T.gpu_run(W, H, fr, L, S, mode="stream", batch=3)
+    fm = T.gpu_run(W, H, fr, L, S, mode="frame")
+    assert np.array_equal(st[0], fr[0])
+    for k in range(1, 5):
+        T.assert_close_f32(st[k], ref[k], integer_scale=float(S).is_integer())
+        assert np.array_equal(st[k], fm[k])
