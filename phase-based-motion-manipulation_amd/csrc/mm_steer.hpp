@@ -144,20 +144,11 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles_wl<LOG2N>(wtw, t0, tw);   // the wave-local transform's bases
+    preload_twiddles<LOG2N>(wtw, t0, tw);
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
     const int kx0 = blk * GPW;
-    // Staging of the band's list rows [0, Hn) for the row-major stores, row k
-    // at slot(k) GPW + grp.  The wave-local inverse leaves bins permuted
-    // (fft_bin: a wave's lanes hold rows C apart), so rows are stored
-    // residue-major, slot(k) = (k mod C) R + k / C (R = ceil(Hn / C) + 4):
-    // a wave's writes land on consecutive slots, the stores' reads of
-    // consecutive rows on C regions 4 slots out of step.
-    c2 *stg = lds_all;
-    constexpr int CW = fft_c_v(LOG2N);
-    const int R = CW == 1 ? g.Hn : (g.Hn + CW - 1) / CW + 4;
-    auto sb_slot = [&](int k) { return CW == 1 ? k : (k % CW) * R + k / CW; };
+    c2 *stg = lds_all;   // [Hn][GPW]
     // Bands level-major (b = o nmid + i - 1 as before): the radial mask of a
     // level is evaluated once for its O/2 orientation bands, which then only
     // add the angular factor (the same expressions per band: bitwise the
@@ -174,7 +165,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             wt[q] = wtw[q];
-            if (tw_slot_used_wl(LOG2N, q)) asm volatile("" : "+v"(wt[q]));
+            if (tw_slot_used(LOG2N, q)) asm volatile("" : "+v"(wt[q]));
         }
         // workgroup-uniform: skip the band where all its columns are zero
         bool all_zero = true;
@@ -198,15 +189,12 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
             }
             v[j] = scale(v0[j], m);
         }
-        // wave-local inverse (fft_dit's counterpart fft_dif: natural order in,
-        // bins permuted out; one workgroup barrier per transform instead of
-        // the all-workgroup Stockham form's six at N = 2048)
-        fft_dif<LOG2N, +1>(v, t, lds, wt);
-        __syncthreads();   // every wave past its exchange reads: the staging overwrites them
+        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
+        // every group has passed the barrier after its last exchange read
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int k = (fft_bin<LOG2N>(t, j) - g.rb + 2 * N) & (N - 1);
-            if (k < g.Hn) stg[sb_slot(k) * GPW + grp] = v[j];
+            const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
+            if (k < g.Hn) stg[k * GPW + grp] = v[j];
         }
         __syncthreads();
         c2 *out = Tb + (size_t)b * band_stride;
@@ -215,12 +203,12 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
             for (int e = grp * T + t; e < g.Hn * PW; e += GPW * T) {
                 const int k = e / PW, part = e - k * PW;
                 *reinterpret_cast<float4 *>(out + (size_t)k * N + kx0 + 2 * part) =
-                    reinterpret_cast<const float4 *>(stg)[sb_slot(k) * PW + part];
+                    reinterpret_cast<const float4 *>(stg)[e];
             }
         } else {                    // tiny N: fewer columns than groups
             for (int e = grp * T + t; e < g.Hn * GPW; e += GPW * T) {
                 const int k = e / GPW, c = e - k * GPW;
-                if (kx0 + c < N) out[(size_t)k * N + kx0 + c] = stg[sb_slot(k) * GPW + c];
+                if (kx0 + c < N) out[(size_t)k * N + kx0 + c] = stg[e];
             }
         }
         __syncthreads();   // the next band's FFT rewrites the buffers
@@ -244,17 +232,6 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 // are 1,084 four-wave workgroups: at 4 waves per SIMD 1,024 of them run at
 // once and the last 60 make a second round of the whole row time; at 5 they
 // all fit one round.
-// MM_SB_ROWS_WL (default 1): the row transforms run wave-local (fft_dif:
-// natural order in, bins permuted out; 2 workgroup barriers per band instead
-// of the all-workgroup Stockham form's 6 at N = 2048), so each thread's bins
-// are columns fft_bin(t, j), and the state planes are kept by register
-// position (t + jT) over all N columns of a row (coalesced; the columns
-// outside the blur window are never read or written): sb_state_cols.
-#ifndef MM_SB_ROWS_WL
-#define MM_SB_ROWS_WL 1
-#endif
-__host__ __device__ constexpr int sb_state_cols(int W, int N) { return MM_SB_ROWS_WL ? N : W + 4; }
-
 template <int LOG2N, bool IIR>
 __global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
@@ -272,17 +249,10 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
     constexpr bool iir = IIR;
-    constexpr bool WL = MM_SB_ROWS_WL;
-    const int SC = sb_state_cols(g.W, N);   // state floats per list row
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    // forward bases (the transforms conjugate them)
-    if constexpr (WL) preload_twiddles_wl<LOG2N>(wtw, t0, tw);
-    else preload_twiddles<LOG2N>(wtw, t0, tw);
-    // column of register j and its state slot (xi < Wc: inside the blur window)
-    auto col = [&](int t, int j) { return WL ? fft_bin<LOG2N>(t, j) : t + j * T; };
-    auto slot = [&](int t, int j, int xi) { return WL ? t + j * T : xi; };
+    preload_twiddles<LOG2N>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
     // row k of band b (contiguous) and its state: loaded one band ahead
     c2 v[8];
     float pp[8], puh[8], pul[8];
@@ -294,16 +264,14 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     };
     auto load_state = [&](int b, int t) {
         if (b < nb && !reset) {
-            const size_t rs = ((size_t)b * g.Hn + k) * SC;
+            const size_t rs = ((size_t)b * g.Hn + k) * Wc;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int xi = (col(t, j) - xs + N) & (N - 1);
-                const bool in = !WL || xi < Wc;   // WL: no state outside the window
-                const int e = slot(t, j, min(xi, Wc - 1));
-                pp[j] = in ? st_phi[rs + e] : 0.0f;
+                const int xi = min((t + j * T - xs + N) & (N - 1), Wc - 1);
+                pp[j] = st_phi[rs + xi];
                 if (iir) {
-                    puh[j] = in ? st_uh[rs + e] : 0.0f;
-                    pul[j] = in ? st_ul[rs + e] : 0.0f;
+                    puh[j] = st_uh[rs + xi];
+                    pul[j] = st_ul[rs + xi];
                 }
             }
         }
@@ -324,15 +292,9 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             wt[i] = wtw[i];
-            if (WL ? tw_slot_used_wl(LOG2N, i) : tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
+            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
         }
-        if constexpr (WL) {
-            // the previous band's inner passes still use the other waves' regions
-            if (b > 0) __syncthreads();
-            fft_dif<LOG2N, +1>(v, t, lds, wt);
-        } else {
-            fft_regs_w<LOG2N, +1>(v, t, lds, wt);
-        }
+        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
         if (b == nb) {   // residual: Hermitian, real output
 #pragma unroll
             for (int j = 0; j < 8; ++j) y[j] += v[j].x;
@@ -370,22 +332,21 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
                 const float rev = P * sp.S_rev;
                 s2 = mul_c(v[j], mk(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)));
             }
-            const int xi = (col(t, j) - xs + N) & (N - 1);
+            const int xi = (t + j * T - xs + N) & (N - 1);
             if (xi < Wc) y[j] += 2.0f * s2.x;
         }
         load_row(b + 1, t);
         __builtin_amdgcn_sched_barrier(0);   // row loads of b+1 ahead of the stores of b
         if (valid) {
-            const size_t rs = ((size_t)b * g.Hn + k) * SC;
+            const size_t rs = ((size_t)b * g.Hn + k) * Wc;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int xi = (col(t, j) - xs + N) & (N - 1);
+                const int xi = (t + j * T - xs + N) & (N - 1);
                 if (xi < Wc) {
-                    const int e = slot(t, j, xi);
-                    st_phi[rs + e] = nph[j];
+                    st_phi[rs + xi] = nph[j];
                     if (iir) {
-                        st_uh[rs + e] = nuh[j];
-                        st_ul[rs + e] = nul[j];
+                        st_uh[rs + xi] = nuh[j];
+                        st_ul[rs + xi] = nul[j];
                     }
                 }
             }
@@ -396,9 +357,8 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     if (!write_out) return;
     // |y| (ConvertComplexMagToTex) then the horizontal half of ApplyAntiAliasing
     float *raw = reinterpret_cast<float *>(lds);
-    if constexpr (WL) __syncthreads();   // every wave past the residual's inner passes
 #pragma unroll
-    for (int j = 0; j < 8; ++j) raw[col(t0, j)] = fabsf(y[j]);
+    for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[j]);
     __syncthreads();
     if (!valid) return;
     float *out = Yh + (size_t)k * g.W;

@@ -139,9 +139,7 @@ def test_steerable_state_size_follows_filter():
     p = mm355.Params.make(levels=5, mode=mm355.MODE_STEERABLE, orientations=8, temporal_filter=0)
     h = mm355.Handle(W, H, p)
     nb = 3 * 4   # 3 middle levels x O/2 band pairs
-    # one float per list row (H + 4) and column: all N columns by register
-    # position (mm_steer.hpp sb_state_cols; W + 4 with -DMM_SB_ROWS_WL=0)
-    plane = nb * (H + 4) * h.N * 4
+    plane = nb * (H + 4) * (W + 4) * 4
     assert h.state_bytes == plane
     h.set_params(mm355.Params.make(levels=5, mode=mm355.MODE_STEERABLE, orientations=8,
                                    temporal_filter=1))
