@@ -539,3 +539,26 @@ def test_k2_generic_op_vs_oracle(W, H, L, S, notab, monkeypatch):
     for k in range(1, 5):
         T.assert_close_f32(st[k], ref[k], integer_scale=float(S).is_integer())
         assert np.array_equal(st[k], fm[k])
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_c2_1080p_long_stream_vs_oracle():
+    """BASELINE C2 over a 96-frame stream in batches of 40 (every K2 launch
+    shape of the bench: packed-block tail, second-half tails, the prime from
+    the state slot at each batch boundary) against the oracle frame by frame,
+    at the RGBA8 bar (max 1 LSB on <= 0.1 % of values)."""
+    W, H, n = 1920, 1080, 96
+    O.set_threads(16)
+    fr = T.synth(W, H, n, fmt="u8")
+    got = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=40)
+    o = O.Oracle(W, H, levels=5, phase_scale=25.0)
+    off = 0
+    for k in range(n):
+        ref = o.process(fr[k])
+        if k == 0:
+            assert np.array_equal(got[0], fr[0])
+            continue
+        T.assert_close_u8(got[k], ref)
+        off += int((got[k] != ref).sum())
+    assert off <= 1e-3 * (n - 1) * W * H * 4
