@@ -562,3 +562,22 @@ def test_c2_1080p_long_stream_vs_oracle():
         T.assert_close_u8(got[k], ref)
         off += int((got[k] != ref).sum())
     assert off <= 1e-3 * (n - 1) * W * H * 4
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_c3_2160p_stream_with_tails_vs_oracle():
+    """BASELINE C3 (3840x2160, L = 6: the two-band op at N = 4096) as one
+    30-frame batch, so K2 runs its packed-block and second-half tails,
+    against the oracle frame by frame at the RGBA8 bar."""
+    W, H, n = 3840, 2160, 30
+    O.set_threads(16)
+    fr = T.synth(W, H, n, fmt="u8")
+    got = T.gpu_run(W, H, fr, 6, 25.0, mode="stream", batch=30)
+    o = O.Oracle(W, H, levels=6, phase_scale=25.0)
+    for k in range(n):
+        ref = o.process(fr[k])
+        if k == 0:
+            assert np.array_equal(got[0], fr[0])
+        else:
+            T.assert_close_u8(got[k], ref)
