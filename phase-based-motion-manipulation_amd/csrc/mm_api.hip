@@ -1196,7 +1196,10 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
     h->ktab_mode = -1;
     h->blur = build_blur();
-    h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : 30;
+    // packed-block frames in k_cols_tail: 40 % at N <= 2048 since the prime
+    // became its own instance (same-call 1080p k_cols 7.92-8.00 -> 7.81-7.82 us;
+    // 50 / 60 %: 7.83-7.88 / 7.80-7.90), 30 % at N = 4096 (C3 33.7 vs 34.3 at 40 %)
+    h->k2_tail_pct = getenv("MM_K2_TAIL") ? atoi(getenv("MM_K2_TAIL")) : (N >= 4096 ? 30 : 40);
     // every packed-block frame in k_cols_tail (MM_K2_PKALL=1): what lets a
     // one-column N = 4096 build (-DMM_K2_GROUPS_4K=1) fit two workgroups per
     // CU; same-call no faster at the default shapes (1080p 8.54 vs 8.58 us,
