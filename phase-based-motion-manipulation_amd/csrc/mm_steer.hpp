@@ -111,9 +111,14 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     const int t0 = threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     // columns near kx = 0 and N carry more bands than those near N/2
-    // (band_col_zero): interleave column runs over the XCDs
+    // (band_col_zero): interleave column runs over the XCDs.  Runs of 64
+    // blocks (128 columns): each XCD then owns a heavy and a light part of the
+    // spectrum in each of the launch's two workgroup rounds (same-call at 1080p,
+    // O = 8: k_sb_cols 117.4 (runs of 8) -> 105.7-105.8 us per frame; 2 / 4 /
+    // 16 / 32 / 128: 121.0-121.5 / 115.5-116.0 / 114.5-114.9 / 116.2-116.6 /
+    // 127.6)
 #ifndef MM_SB_COLS_RUN
-#define MM_SB_COLS_RUN 8
+#define MM_SB_COLS_RUN 64
 #endif
     const int blk = xcd_interleave<MM_SB_COLS_RUN>(blockIdx.x, gridDim.x);
     const int kx_raw = blk * GPW + grp;
