@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "phase-based-motion-manipulation_amd"))
 
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+RESIDENT_BYTES = 32 << 30       # cap on the resident input frames (of 288 GB)
 
 
 def metric_name(W, H, L, orientations=1, standard=False):
@@ -179,6 +180,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-frames", type=int, default=30, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-keep", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-pairs", default="", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -288,6 +290,17 @@ def _cpu_worker(a):
         if time.perf_counter() - t0 >= a.cpu_seconds:
             break
     dt = time.perf_counter() - t0
+    pairs = [int(t) for t in a.cpu_pairs.split(",")] if a.cpu_pairs else []
+    if pairs:
+        # untimed: the output of frame t needs only frames t-1 and t (.cs:142),
+        # so the launch-boundary frames of the timed step come from a reset
+        # oracle fed those two frames
+        po = []
+        for t in pairs:
+            o.reset()
+            o.process(O.synth_frame(W, H, t - 1))
+            po.append(o.process(O.synth_frame(W, H, t)))
+        np.save(a.cpu_out + ".pairs.npy", np.stack(po))
     o.close()
     if a.cpu_keep:
         np.save(a.cpu_out + ".npy", np.stack(outs))
@@ -307,7 +320,7 @@ def cpu_baseline(a):
     W, H, L, S = a.width, a.height, a.levels, a.phase_scale
     cores = available_cpus()
 
-    def run(threads, max_frames, seconds, keep):
+    def run(threads, max_frames, seconds, keep, pairs=()):
         with tempfile.TemporaryDirectory() as d:
             out = os.path.join(d, "cpu.json")
             env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close",
@@ -318,15 +331,20 @@ def cpu_baseline(a):
                    "--levels", str(L), "--phase-scale", str(S)]
             if keep:
                 cmd.append("--cpu-keep")
+            if pairs:
+                cmd += ["--cpu-pairs", ",".join(str(t) for t in pairs)]
             if a.standard:
                 cmd.append("--standard")
-            subprocess.run(cmd, env=env, check=True, timeout=seconds * 4 + 120)
+            subprocess.run(cmd, env=env, check=True, timeout=seconds * 4 + 240)
             rec = json.load(open(out))
             outs = np.load(out + ".npy") if keep else None
-        return rec["threads"], rec["frames"], rec["seconds"], outs
+            pouts = np.load(out + ".pairs.npy") if pairs else None
+        return rec["threads"], rec["frames"], rec["seconds"], outs, pouts
 
-    thr, n, dt, outs = run(cores, 30, a.cpu_seconds, True)
-    _, n1, dt1, _ = run(1, 30, a.cpu_seconds / 3, False)
+    pairs = boundary_frames(a.frames_per_step, min(a.batch or a.frames_per_step, a.frames_per_step),
+                            W, H)
+    thr, n, dt, outs, pouts = run(cores, 30, a.cpu_seconds, True, pairs)
+    _, n1, dt1, _, _ = run(1, 30, a.cpu_seconds / 3, False)
     rec = {"value": round(n / dt, 4), "unit": "frames/s", "cores": thr, "kind": "port",
            "single_thread_value": round(n1 / dt1, 4), "single_thread_frames": n1,
            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(), "cpus_available": cores,
@@ -337,27 +355,57 @@ def cpu_baseline(a):
                      f"OpenMP {thr} threads (every CPU available to this job: affinity mask "
                      f"and cgroup quota; the host shows {os.cpu_count()}); single-thread on "
                      f"t=1..{n1}"}
-    return rec, outs
+    return rec, (outs, pairs, pouts)
 
 
-def parity_check(mm355, torch, params, W, H, ref, local):
-    """The oracle's frames 0..n (cpu_baseline) against a fresh handle on the
-    same synthetic frames generated on the device (SURVEY.md §8c RGBA8 bar:
-    exact except +-1 LSB on <= 0.1% of values; frame 0 bitwise)."""
+def boundary_frames(C, B, W, H):
+    """The frames of a C-frame step in batches of B where K2's launch shape
+    changes (mm_api.hip launch_k2): each batch's first frames (the prime from
+    the state slot), the packed block's hand-off to k_cols_tail (40 % of the
+    batch at N <= 2048, 30 % at N = 4096), the second-half blocks' tails (10 %)
+    and each batch's last frame.  Frames 1..30 are checked in sequence anyway."""
+    N = 1
+    while N < max(W, H):
+        N *= 2
+    tail_pct = 30 if N >= 4096 else 40
+    out = set()
+    for b in range(0, C, B):
+        nf = min(B, C - b)
+        k = max(0, min(nf * tail_pct // 100, nf - 2)) if nf >= 24 else 0
+        k2t = min(nf * 10 // 100, nf - 2) if nf >= 24 else 0
+        for t in (b, b + 1, b + nf - k - 1, b + nf - k, b + nf - k2t - 1, b + nf - k2t, b + nf - 1):
+            if 31 <= t < C:
+                out.add(t)
+    return sorted(out)
+
+
+def parity_check(mm355, torch, params, W, H, ref, local, C, B):
+    """The timed step itself against the oracle: a fresh handle at the timed
+    batch B processes the step's C frames (one mm_process_stream call, the
+    same launch shapes as the timed region: K2's prime, packed-block and
+    second-half tails), and its output frames 0..n (the oracle's sequential
+    run in cpu_baseline) and every launch-boundary frame (boundary_frames:
+    the oracle fed frames t-1, t) are held to SURVEY.md §8c's RGBA8 bar:
+    exact except +-1 LSB on <= 0.1% of values; frame 0 bitwise."""
     import numpy as np
-    n = ref.shape[0]
+    seq, pairs, pref = ref
+    n = seq.shape[0]
     h = mm355.Handle(W, H, params, device=local)
-    h.set_batch(n)
-    fr = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    h.set_batch(B)
+    fr = torch.empty((C, H, W, 4), dtype=torch.uint8, device="cuda")
     out = torch.empty_like(fr)
     st = torch.cuda.current_stream().cuda_stream
-    h.synth(fr, 0, n, seed=0x5EED0000, stream=st)
-    h.process_stream(fr, out, n, mm355.RGBA8, stream=st)
+    h.synth(fr, 0, C, seed=0x5EED0000, stream=st)
+    h.process_stream(fr, out, C, mm355.RGBA8, stream=st)
     torch.cuda.synchronize()
-    got = out.cpu().numpy()
+    idx = list(range(n)) + list(pairs)
+    got = out[idx].cpu().numpy()
     h.close()
-    d = np.abs(got.astype(np.int16) - ref.astype(np.int16))
-    return {"frames": int(n), "first_frame_bitwise": bool(np.array_equal(got[0], ref[0])),
+    want = np.concatenate([seq, pref]) if len(pairs) else seq
+    d = np.abs(got.astype(np.int16) - want.astype(np.int16))
+    return {"frames": len(idx), "sequence": f"0..{n - 1}", "boundary_frames": list(pairs),
+            "launch_shape": f"{C} frames in one call, batches of {B} (the timed step)",
+            "first_frame_bitwise": bool(np.array_equal(got[0], seq[0])),
             "max_abs_lsb": int(d.max()), "frac_values_off": float((d > 0).mean()),
             "rmse_lsb": round(float(np.sqrt((d.astype(np.float64) ** 2).mean())), 5),
             "bar": "max 1 LSB, <= 0.1% of values"}
@@ -510,13 +558,18 @@ def main():
     h.set_batch(B)
     N = h.N
 
-    # resident inputs: one buffer per step (warmup + timed), generated on device
+    # resident inputs: one buffer per step (warmup + timed), generated on
+    # device, at most RESIDENT_BYTES of them (4K x 25 steps would take 249 GB
+    # of the 288 GB): step s then reads buffer s mod nbuf, which holds
+    # frames of an earlier step; every step still moves all of its bytes
     total_steps = a.warmup + a.steps
     ring = a.mode == "ring" and world > 1 and not c_ring
     replica = rank if a.replica_index is None else a.replica_index
     seed = 0x5EED0000 + (0 if a.mode == "ring" else replica)
-    frames = torch.empty((total_steps, C, H, W, 4), dtype=torch.uint8, device="cuda")
-    for s in range(total_steps):
+    step_bytes = C * H * W * 4
+    nbuf = max(2, min(total_steps, RESIDENT_BYTES // step_bytes))
+    frames = torch.empty((nbuf, C, H, W, 4), dtype=torch.uint8, device="cuda")
+    for s in range(nbuf):
         t0 = (s * world * C + rank * C) if a.mode == "ring" else s * C
         h.synth(frames[s], t0, C, seed=seed, stream=torch.cuda.current_stream().cuda_stream)
     out = torch.empty((C, H, W, 4), dtype=torch.uint8, device="cuda")
@@ -542,8 +595,8 @@ def main():
         if cring is None:
             stream.step(s, prefetch=ring and s + 1 < total_steps)
             return
-        nxt = frames[s + 1, C - 1] if s + 1 < total_steps else None
-        cring.step(s, frames[s], out, nxt, stream=torch.cuda.current_stream().cuda_stream)
+        nxt = frames[(s + 1) % nbuf, C - 1] if s + 1 < total_steps else None
+        cring.step(s, frames[s % nbuf], out, nxt, stream=torch.cuda.current_stream().cuda_stream)
         if backend.sums is not None:
             v = out.reshape(C, -1).sum(dim=1, dtype=torch.int64).cpu()
             lo = s * world * C + rank * C
@@ -687,7 +740,7 @@ def main():
                                                         local, a.drop_in_frames)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not steer:
         result["cpu_baseline"], ref = cpu_baseline(a)
-        result["parity_vs_oracle"] = parity_check(mm355, torch, params, W, H, ref, local)
+        result["parity_vs_oracle"] = parity_check(mm355, torch, params, W, H, ref, local, C, B)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

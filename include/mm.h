@@ -140,7 +140,10 @@ int mm_padded_size(const mm_handle *h, int *n);
  * HIP; mm_stream(h) is a non-blocking stream owned by the handle); otherwise
  * in/out are host pointers and the call returns when out is written.
  * Every device-pointer entry point below orders its work on `hip_stream` the
- * same way: a caller that produced the input on another stream synchronises. */
+ * same way: a caller that produced the input on another stream synchronises.
+ * A call on a different stream than the handle's previous call first makes
+ * that stream wait for the previous call's work (since ABI 9: calls of one
+ * handle never overlap, whatever streams they use). */
 int mm_process(mm_handle *h, const void *in, void *out, int format, int flags,
                void *hip_stream);
 
@@ -210,7 +213,16 @@ int mm_release_frames(mm_ext_frames *x);
  * that work only, never for the whole device: other handles and streams on
  * the GPU keep running.  Work the CALLER queued on its streams that reads
  * handle-owned memory (none through this API: frames are caller-owned) is the
- * caller's to finish first.  Since ABI 9. */
+ * caller's to finish first.  Since ABI 9.
+ * Hardware-queue caveat (this and mm_set_params / mm_set_batch): the HIP
+ * runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4)
+ * round-robin, and streams that share a hardware queue execute in one order.
+ * With more live streams than queues, this handle's stream can sit behind
+ * another stream's blocked work on the same queue, and the wait for "this
+ * handle's own work" then also waits for that work.  The entry point itself
+ * never synchronises the device; a process that must not couple streams that
+ * way raises GPU_MAX_HW_QUEUES (tests/test_handle.py runs its no-stall tests
+ * with 16). */
 void mm_destroy(mm_handle *h);
 
 const char *mm_strerror(int code);

@@ -58,6 +58,26 @@ int mm_ring_create(int world, int rank, const unsigned char id[MM_RING_ID_BYTES]
 int mm_ring_step(mm_ring *r, int step, const void *in, void *out, const void *next_last,
                  void *hip_stream);
 
+/* MM_MODE_STEERABLE with MM_FILTER_IIR ("a recursive IIR
+ * extension ... would need a warm-up halo").  The IIR state after frame t is a
+ * history of every frame before it, so no single frame's state can be handed
+ * to the next rank without serialising the ring.  Instead each rank restarts
+ * its filter from rest `halo_frames` frames before its chunk: `halo` = the
+ * input frames [c - halo_frames, c) immediately preceding the chunk's first
+ * frame c (device memory, caller-owned: the caller reads them from its source
+ * as it reads the chunk), processed with their outputs discarded, then the
+ * chunk into `out`.  halo_frames = min(c, mm_ring_halo_frames()) (the halo of
+ * a chunk near the stream's start begins at frame 0, which is then exact;
+ * rank 0 of step 0 passes 0).  The filter's two poles decay by (1 - iir_high)
+ * and (1 - iir_low) per frame, so the difference from the single-rank stream
+ * falls as (1 - iir_low)^halo_frames: mm_ring_halo_frames() picks the halo at
+ * which that factor is 1e-6 (270 frames at iir_low = 0.05), where RGBA8
+ * outputs meet the parity bar (<= 1 LSB on <= 0.1 % of values; tests/test_ring_c.py).
+ * Nothing crosses the ring in this mode.  mm_ring_step refuses IIR handles. */
+int mm_ring_step_halo(mm_ring *r, int step, const void *halo, int halo_frames, const void *in, void *out,
+                      void *hip_stream);
+int mm_ring_halo_frames(const mm_ring *r, int *frames);
+
 /* Waits for every posted shift (a shift posted for a step that is never run
  * included) and releases the ring. */
 void mm_ring_destroy(mm_ring *r);

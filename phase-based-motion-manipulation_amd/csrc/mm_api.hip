@@ -69,6 +69,7 @@ struct mm_handle {
     hipEvent_t last_ev;         // recorded after this handle's latest work (mm_set_params)
     hipEvent_t retire_ev;       // orders a buffer's return to the pool behind a call's stream
     bool last_ev_set;
+    hipStream_t last_s;         // the stream last_ev was recorded on
     bool k2_tab;                // pyramid masks from the per-bin LDS table (<= 2 bands/bin)
     int k2_sp;                  // ... and the phase factor as z^S, |S| == k2_sp (k_cols SP; 0: atan2)
     bool k2_tab2;               // ... with overlapping middle bands (MM_K2_PYR_TAB2)
@@ -154,6 +155,17 @@ static int note_work(mm_handle *h, hipStream_t s)
 {
     HIPCHK(hipEventRecord(h->last_ev, s));
     h->last_ev_set = true;
+    h->last_s = s;
+    return MM_OK;
+}
+
+// A call on another stream than the handle's previous call first waits for
+// that call's work (last_ev), so last_ev always covers every earlier call and
+// the buffers h_retire returns behind it are not still read on the old stream.
+// Same stream (the one-frame drop-in pattern): nothing to do.
+static int order_after_last(mm_handle *h, hipStream_t s)
+{
+    if (h->last_ev_set && s != h->last_s) HIPCHK(hipStreamWaitEvent(s, h->last_ev, 0));
     return MM_OK;
 }
 
@@ -1071,8 +1083,8 @@ static int alloc_batch(mm_handle *h, int frames)
     }
     if (h->d_G && h->g_valid) {
         // behind the handle's last work (which may still be writing the slot)
-        if (h->last_ev_set) HIPCHK(hipStreamWaitEvent(h->stream, h->last_ev, 0));
-        if (hipMemcpyAsync(G + h->g_stride * frames, h->d_G + h->g_stride * h->gs, sizeof(c2) * h->g_stride,
+        if ((h->last_ev_set && hipStreamWaitEvent(h->stream, h->last_ev, 0) != hipSuccess) ||
+            hipMemcpyAsync(G + h->g_stride * frames, h->d_G + h->g_stride * h->gs, sizeof(c2) * h->g_stride,
                            hipMemcpyDeviceToDevice, h->stream) != hipSuccess) {
             h_retire(h, G);
             h_retire(h, Q);
@@ -1333,6 +1345,8 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
     if (count == 0) return MM_OK;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
+    int ro = order_after_last(h, s);
+    if (ro) return ro;
     // last_ev also after a failed call: kernels it launched before failing may
     // still read the handle's buffers
     const int rc = do_stream(h, (const uint8_t *)in, (uint8_t *)out, count, format, s);
@@ -1349,6 +1363,8 @@ int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, v
     const size_t fb = (size_t)h->W * h->H * (format ? 16 : 4);
     DEVICE_SCOPE(h);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    int ro = order_after_last(h, s);
+    if (ro) return ro;
     if (h->stage_bytes < fb) {
         h_retire(h, h->d_stage_in, s, true);
         h_retire(h, h->d_stage_out, s, true);
@@ -1392,12 +1408,14 @@ int mm_get_state(mm_handle *h, void *dev_buf, size_t bytes, void *hip_stream)
     if (!h->has_state) return MM_ERR_NO_STATE;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
+    if (h->p.mode == MM_MODE_STEERABLE && !h->steer_valid) return MM_ERR_NO_STATE;
+    if (h->p.mode != MM_MODE_STEERABLE && !h->g_valid) return MM_ERR_NO_STATE;
+    int ro = order_after_last(h, s);
+    if (ro) return ro;
     if (h->p.mode == MM_MODE_STEERABLE) {
-        if (!h->steer_valid) return MM_ERR_NO_STATE;
         HIPCHK(hipMemcpyAsync(dev_buf, h->d_sst, need, hipMemcpyDeviceToDevice, s));
         return note_work(h, s);
     }
-    if (!h->g_valid) return MM_ERR_NO_STATE;
     HIPCHK(hipMemcpyAsync(dev_buf, h->d_G + h->g_stride * h->gs, need, hipMemcpyDeviceToDevice, s));
     return note_work(h, s);
 }
@@ -1408,14 +1426,18 @@ int mm_set_state(mm_handle *h, const void *dev_buf, size_t bytes, void *hip_stre
     if (!h || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
+    int ro = order_after_last(h, s);
+    if (ro) return ro;
     if (h->p.mode == MM_MODE_STEERABLE) {
         int rc = steer_alloc(h, s);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(h->d_sst, dev_buf, need, hipMemcpyDeviceToDevice, s));
         h->steer_valid = true;
+        h->g_valid = false;   // the G slot still holds an earlier, unrelated frame
         h->has_state = true;
         return note_work(h, s);
     }
+    h->steer_valid = false;   // the local-phase planes belong to an earlier frame
     h->gs = h->chunk;   // the spare slot: between calls no batch occupies G
     HIPCHK(hipMemcpyAsync(h->d_G + h->g_stride * h->gs, dev_buf, need, hipMemcpyDeviceToDevice, s));
     h->has_state = true;
@@ -1434,6 +1456,8 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
     // the IIR state is a history of frames, not a function of one input frame
     if (h->p.mode == MM_MODE_STEERABLE && h->p.temporal_filter == MM_FILTER_IIR)
         return MM_ERR_UNSUPPORTED;
+    int ro = order_after_last(h, s);
+    if (ro) return ro;
     const int rc = do_compute_state(h, (const uint8_t *)in_dev, format, dev_buf, s);
     const int rn = note_work(h, s);
     return rc ? rc : rn;

@@ -9,8 +9,16 @@
  *   mm_cli [-w W] [-h H] [-n frames] [-l levels] [-s phase_scale]
  *          [-b frames_per_call] [-i in.{rgba,y4m}] [-o out.{rgba,y4m}] [-d device]
  *          [--full-range] [--standard] [--show-magnitude] [--show-phase]
+ *          [--orientations O] [--iir] [--halo K]
  *          [--checksum] [--ring-world G --ring-rank R --ring-id FILE]
- *          [--ring-local G]
+ *          [--ring-local G [--compare]]
+ *
+ * --orientations O (4/6/8): MM_MODE_STEERABLE extension,
+ * DIFF temporal filter, or IIR with --iir.  A sharded IIR stream warms each
+ * rank's filter on the halo of frames before its chunk (mm_ring_step_halo;
+ * --halo K overrides mm_ring_halo_frames()).  --compare (with --ring-local):
+ * the single-handle stream afterwards, frame by frame against the ring's
+ * outputs ("cmp t maxabs ndiff" lines and a summary).
  *
  * --ring-*: frame-sharded synthetic stream over an RCCL ring (include/mm_ring.h,
  * SURVEY.md §8e), one process per GPU: rank R of G processes chunks of -b
@@ -127,7 +135,7 @@ static int ring_id(int rank, const char *path, unsigned char id[MM_RING_ID_BYTES
 /* Frame-sharded synthetic stream: rank R of G owns frames
  * [s*G*B + R*B, s*G*B + (R+1)*B) of step s. */
 static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world, int rank,
-                    const char *id_path, int checksum)
+                    const char *id_path, int checksum, int halo)
 {
     unsigned char id[MM_RING_ID_BYTES];
     if (ring_id(rank, id_path, id)) {
@@ -141,9 +149,12 @@ static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world
         return 1;
     }
     const size_t fb = (size_t)W * H * 4;
-    void *d_in = NULL, *d_out = NULL, *d_next = NULL;
+    void *d_in = NULL, *d_out = NULL, *d_next = NULL, *d_halo = NULL;
+    int K = 0;
+    if (mm_ring_halo_frames(r, &K)) return 1;
+    if (halo >= 0 && K > 0) K = halo;
     if (hipMalloc(&d_in, fb * B) != hipSuccess || hipMalloc(&d_out, fb * B) != hipSuccess ||
-        hipMalloc(&d_next, fb) != hipSuccess) {
+        hipMalloc(&d_next, fb) != hipSuccess || (K > 0 && hipMalloc(&d_halo, fb * K) != hipSuccess)) {
         fprintf(stderr, "hipMalloc failed\n");
         return 1;
     }
@@ -158,8 +169,11 @@ static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world
         CHECK(mm_synth_frames(d_in, W, H, t0, B, 0x5EED0000ull, 0, s));
         const int last = st + 1 < steps;
         if (last) CHECK(mm_synth_frames(d_next, W, H, t0 + world * B + B - 1, 1, 0x5EED0000ull, 0, s));
+        const int hk = t0 < K ? t0 : K;   /* IIR: the warm-up halo before the chunk */
+        if (hk) CHECK(mm_synth_frames(d_halo, W, H, t0 - hk, hk, 0x5EED0000ull, 0, s));
         hipEventRecord(e0, s);
-        rc = mm_ring_step(r, st, d_in, d_out, last ? d_next : NULL, s);
+        rc = K > 0 ? mm_ring_step_halo(r, st, d_halo, hk, d_in, d_out, s)
+                   : mm_ring_step(r, st, d_in, d_out, last ? d_next : NULL, s);
         if (rc) {
             fprintf(stderr, "mm_ring_step: %s (%s)\n", mm_strerror(rc), mm_ring_last_error());
             return 1;
@@ -178,6 +192,7 @@ static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world
     hipFree(d_in);
     hipFree(d_out);
     hipFree(d_next);
+    hipFree(d_halo);
     return 0;
 }
 
@@ -185,8 +200,9 @@ static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world
 typedef struct {
     mm_ring_hub *hub;
     const mm_params *p;
-    int W, H, F, B, dev, world, rank, checksum;
+    int W, H, F, B, dev, world, rank, checksum, halo;
     uint64_t *hashes;   /* [F], global frame index */
+    unsigned char *d_all;   /* --compare: every output frame, global index (device) */
     int rc;
     char err[256];
 } local_rank;
@@ -210,8 +226,12 @@ static void *local_rank_main(void *arg)
         fprintf(stderr, "rank %d: %s\n", a->rank, a->err);
         exit(1);
     }
+    int K = 0;
+    void *d_halo = NULL;
+    if (mm_ring_halo_frames(r, &K)) exit(1);
+    if (a->halo >= 0 && K > 0) K = a->halo;
     if (hipMalloc(&d_in, fb * a->B) != hipSuccess || hipMalloc(&d_out, fb * a->B) != hipSuccess ||
-        hipMalloc(&d_next, fb) != hipSuccess) {
+        hipMalloc(&d_next, fb) != hipSuccess || (K > 0 && hipMalloc(&d_halo, fb * K) != hipSuccess)) {
         fprintf(stderr, "rank %d: hipMalloc failed\n", a->rank);
         exit(1);
     }
@@ -225,8 +245,16 @@ static void *local_rank_main(void *arg)
             fprintf(stderr, "rank %d: mm_synth_frames: %s\n", a->rank, mm_strerror(rc));
             exit(1);
         }
-        if ((rc = mm_ring_step(r, st, d_in, d_out, more ? d_next : NULL, s))) {
+        const int hk = t0 < K ? t0 : K;   /* IIR: the warm-up halo before the chunk */
+        if (hk && (rc = mm_synth_frames(d_halo, a->W, a->H, t0 - hk, hk, 0x5EED0000ull, 0, s))) exit(1);
+        if ((rc = K > 0 ? mm_ring_step_halo(r, st, d_halo, hk, d_in, d_out, s)
+                        : mm_ring_step(r, st, d_in, d_out, more ? d_next : NULL, s))) {
             fprintf(stderr, "rank %d: mm_ring_step: %s (%s)\n", a->rank, mm_strerror(rc), mm_ring_last_error());
+            exit(1);
+        }
+        if (a->d_all && hipMemcpyAsync(a->d_all + fb * (size_t)t0, d_out, fb * a->B, hipMemcpyDeviceToDevice, s) !=
+                            hipSuccess) {
+            fprintf(stderr, "rank %d: keep outputs\n", a->rank);
             exit(1);
         }
         if (a->checksum) {
@@ -243,11 +271,60 @@ static void *local_rank_main(void *arg)
     hipFree(d_in);
     hipFree(d_out);
     hipFree(d_next);
+    hipFree(d_halo);
     a->rc = 0;
     return NULL;
 }
 
-static int run_ring_local(const mm_params *p, int W, int H, int F, int B, int dev, int world, int checksum)
+/* --compare: the same stream through one handle in calls of B frames, frame
+ * by frame against the ring's outputs: "cmp t maxabs ndiff" per frame and a
+ * summary line (the IIR halo's tolerance, tests/test_ring_c.py) */
+static int compare_single(const mm_params *p, int W, int H, int F, int B, int dev, const unsigned char *d_all)
+{
+    const size_t fb = (size_t)W * H * 4;
+    mm_handle *h = NULL;
+    void *d_in = NULL, *d_out = NULL;
+    unsigned char *a = (unsigned char *)malloc(fb), *b = (unsigned char *)malloc(fb);
+    if (!a || !b) return 1;
+    CHECK(mm_create(W, H, p, dev, &h));
+    CHECK(mm_set_batch(h, B));
+    if (hipMalloc(&d_in, fb * B) != hipSuccess || hipMalloc(&d_out, fb * B) != hipSuccess) return 1;
+    hipStream_t s = (hipStream_t)mm_stream(h);
+    long long ndiff_all = 0;
+    int max_all = 0;
+    for (int f0 = 0; f0 < F; f0 += B) {
+        CHECK(mm_synth_frames(d_in, W, H, f0, B, 0x5EED0000ull, 0, s));
+        CHECK(mm_process_stream(h, d_in, d_out, B, MM_RGBA8, s));
+        if (hipStreamSynchronize(s) != hipSuccess) return 1;
+        for (int k = 0; k < B; ++k) {
+            if (hipMemcpy(a, (unsigned char *)d_out + fb * k, fb, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(b, d_all + fb * (size_t)(f0 + k), fb, hipMemcpyDeviceToHost) != hipSuccess)
+                return 1;
+            int mx = 0;
+            long long nd = 0;
+            for (size_t i = 0; i < fb; ++i) {
+                const int d = a[i] > b[i] ? a[i] - b[i] : b[i] - a[i];
+                if (d) {
+                    ++nd;
+                    if (d > mx) mx = d;
+                }
+            }
+            printf("cmp %d %d %lld\n", f0 + k, mx, nd);
+            ndiff_all += nd;
+            if (mx > max_all) max_all = mx;
+        }
+    }
+    printf("compare frames %d maxabs %d ndiff %lld values %lld\n", F, max_all, ndiff_all, (long long)fb * F);
+    mm_destroy(h);
+    hipFree(d_in);
+    hipFree(d_out);
+    free(a);
+    free(b);
+    return 0;
+}
+
+static int run_ring_local(const mm_params *p, int W, int H, int F, int B, int dev, int world, int checksum,
+                          int halo, int compare)
 {
     if (world < 1 || world > 64 || F % (world * B) != 0) {
         fprintf(stderr, "--ring-local: need 1 <= G <= 64 and frames a multiple of G * batch\n");
@@ -259,6 +336,13 @@ static int run_ring_local(const mm_params *p, int W, int H, int F, int B, int de
     local_rank *ranks = (local_rank *)calloc((size_t)world, sizeof(local_rank));
     pthread_t *th = (pthread_t *)calloc((size_t)world, sizeof(pthread_t));
     if (!hashes || !ranks || !th) return 1;
+    unsigned char *d_all = NULL;
+    if (compare) {
+        if (hipSetDevice(dev) != hipSuccess || hipMalloc((void **)&d_all, (size_t)W * H * 4 * (size_t)F) != hipSuccess) {
+            fprintf(stderr, "--compare: hipMalloc of %d frames failed\n", F);
+            return 1;
+        }
+    }
     for (int g = 0; g < world; ++g) {
         local_rank *a = &ranks[g];
         a->hub = hub;
@@ -266,6 +350,8 @@ static int run_ring_local(const mm_params *p, int W, int H, int F, int B, int de
         a->W = W; a->H = H; a->F = F; a->B = B; a->dev = dev;
         a->world = world; a->rank = g; a->checksum = checksum;
         a->hashes = hashes;
+        a->halo = halo;
+        a->d_all = d_all;
         if (pthread_create(&th[g], NULL, local_rank_main, a) != 0) {
             fprintf(stderr, "pthread_create failed\n");
             exit(1);
@@ -279,6 +365,8 @@ static int run_ring_local(const mm_params *p, int W, int H, int F, int B, int de
     if (!rc && checksum)
         for (int t = 0; t < F; ++t) printf("frame %d %llu\n", t, (unsigned long long)hashes[t]);
     printf("ring-local world %d  steps %d  chunk %d\n", world, F / (world * B), B);
+    if (!rc && compare) rc = compare_single(p, W, H, F, B, dev, d_all);
+    if (d_all) hipFree(d_all);
     mm_ring_hub_destroy(hub);
     free(hashes);
     free(ranks);
@@ -290,7 +378,7 @@ int main(int argc, char **argv)
 {
     int W = 1920, H = 1080, F = 300, L = 5, B = 30, dev = 0;
     int full_range = 0, standard = 0, show_mag = 0, show_phase = 0, checksum = 0;
-    int ring_world = 0, ring_rank = 0, ring_local = 0;
+    int ring_world = 0, ring_rank = 0, ring_local = 0, orientations = 1, iir = 0, halo = -1, compare = 0;
     float S = 25.0f;
     const char *in_path = NULL, *out_path = NULL, *ring_id_path = NULL;
     for (int i = 1; i < argc; ++i) {
@@ -300,6 +388,8 @@ int main(int argc, char **argv)
         if (!strcmp(a, "--show-magnitude")) { show_mag = 1; continue; }
         if (!strcmp(a, "--show-phase")) { show_phase = 1; continue; }
         if (!strcmp(a, "--checksum")) { checksum = 1; continue; }
+        if (!strcmp(a, "--iir")) { iir = 1; continue; }
+        if (!strcmp(a, "--compare")) { compare = 1; continue; }
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
         if (!v) { fprintf(stderr, "missing value for %s\n", a); return 2; }
         if (!strcmp(a, "-w")) W = atoi(v);
@@ -315,6 +405,8 @@ int main(int argc, char **argv)
         else if (!strcmp(a, "--ring-rank")) ring_rank = atoi(v);
         else if (!strcmp(a, "--ring-id")) ring_id_path = v;
         else if (!strcmp(a, "--ring-local")) ring_local = atoi(v);
+        else if (!strcmp(a, "--orientations")) orientations = atoi(v);
+        else if (!strcmp(a, "--halo")) halo = atoi(v);
         else { fprintf(stderr, "unknown option %s\n", a); return 2; }
         ++i;
     }
@@ -336,7 +428,9 @@ int main(int argc, char **argv)
     mm_params_default(&p);
     p.levels = L;
     p.phase_scale = S;
-    p.mode = standard ? MM_MODE_STANDARD : MM_MODE_PYRAMID;
+    p.mode = standard ? MM_MODE_STANDARD : orientations > 1 ? MM_MODE_STEERABLE : MM_MODE_PYRAMID;
+    p.orientations = orientations;
+    p.temporal_filter = iir ? MM_FILTER_IIR : MM_FILTER_DIFF;
     p.show_magnitude = show_mag;
     p.show_phase = show_phase;
     if (ring_local > 0) {
@@ -344,7 +438,7 @@ int main(int argc, char **argv)
             fprintf(stderr, "--ring-local needs a synthetic stream\n");
             return 2;
         }
-        return run_ring_local(&p, W, H, F, B, dev, ring_local, checksum);
+        return run_ring_local(&p, W, H, F, B, dev, ring_local, checksum, halo, compare);
     }
     /* mm_create runs on `dev` and gives the caller's current device back:
      * this program's own buffers, events and default stream must be on `dev`
@@ -364,7 +458,7 @@ int main(int argc, char **argv)
             return 2;
         }
         CHECK(mm_set_batch(h, B));
-        const int rc = run_ring(h, W, H, F, B, dev, ring_world, ring_rank, ring_id_path, checksum);
+        const int rc = run_ring(h, W, H, F, B, dev, ring_world, ring_rank, ring_id_path, checksum, halo);
         mm_destroy(h);
         return rc;
     }

@@ -41,6 +41,7 @@ struct mm_ring {
     void *st_out[2], *st_in[2];   /* per posted step, slot = step & 1 */
     void *carry;                  /* rank 0: st_in of the previous step */
     int posted[2];                /* step posted in the slot, -1: none */
+    int halo_mode;                /* MM_FILTER_IIR steerable: mm_ring_step_halo only */
     hipEvent_t ready[2];          /* st_out written (caller's stream) */
     hipEvent_t done[2];           /* shift finished (ring stream) */
 };
@@ -129,8 +130,6 @@ static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int wid
     mm_params p;
     int rc = mm_get_params(h, &p);
     if (rc) return rc;
-    if (p.mode == MM_MODE_STEERABLE && p.temporal_filter == MM_FILTER_IIR)
-        return MM_ERR_UNSUPPORTED;   /* the IIR state is a history, not one frame's */
     mm_ring *r = (mm_ring *)calloc(1, sizeof *r);
     if (!r) return MM_ERR_OOM;
     r->world = world;
@@ -141,6 +140,9 @@ static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int wid
     r->h = h;
     r->posted[0] = r->posted[1] = -1;
     r->frame_bytes = (size_t)width * height * (format == MM_RGBA8 ? 4 : 16);
+    /* the IIR state is a history of frames, not one frame's function: nothing
+     * is shifted, each rank warms its filter on a halo (mm_ring_step_halo) */
+    r->halo_mode = p.mode == MM_MODE_STEERABLE && p.temporal_filter == MM_FILTER_IIR;
     if ((rc = mm_state_size(h, &r->state_bytes))) {
         release(r);
         return rc;
@@ -151,7 +153,7 @@ static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int wid
         release(r);
         return fail_hip("ring stream", e);
     }
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 2 && !r->halo_mode; ++k) {
         if ((e = hipMalloc(&r->st_out[k], r->state_bytes)) != hipSuccess ||
             (e = hipMalloc(&r->st_in[k], r->state_bytes)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&r->ready[k], hipEventDisableTiming)) != hipSuccess ||
@@ -160,7 +162,7 @@ static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int wid
             return MM_ERR_OOM;
         }
     }
-    if ((e = hipMalloc(&r->carry, r->state_bytes)) != hipSuccess) {
+    if (!r->halo_mode && (e = hipMalloc(&r->carry, r->state_bytes)) != hipSuccess) {
         release(r);
         return MM_ERR_OOM;
     }
@@ -270,6 +272,11 @@ int mm_ring_create_local(mm_ring_hub *hub, int rank, int hip_device, mm_handle *
     hipError_t e;
     if ((e = hipEventCreateWithFlags(&hub->posted[rank], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&hub->copied[rank], hipEventDisableTiming)) != hipSuccess) {
+        /* release() closes the transport only once r->ops is set: the events
+         * created so far are destroyed here */
+        if (hub->posted[rank]) (void)hipEventDestroy(hub->posted[rank]);
+        if (hub->copied[rank]) (void)hipEventDestroy(hub->copied[rank]);
+        hub->posted[rank] = hub->copied[rank] = NULL;
         release(r);
         return fail_hip("local ring events", e);
     }
@@ -325,6 +332,10 @@ int mm_ring_step(mm_ring *r, int step, const void *in, void *out, const void *ne
                  void *hip_stream)
 {
     if (!r || !in || !out || step < 0) return MM_ERR_INVALID;
+    if (r->halo_mode) {
+        snprintf(g_err, sizeof g_err, "IIR steerable handle: use mm_ring_step_halo");
+        return MM_ERR_UNSUPPORTED;
+    }
     hipStream_t s = (hipStream_t)hip_stream;
     HIP_TRY(hipSetDevice(r->device));
     int rc;
@@ -334,3 +345,51 @@ int mm_ring_step(mm_ring *r, int step, const void *in, void *out, const void *ne
 }
 
 void mm_ring_destroy(mm_ring *r) { release(r); }
+
+int mm_ring_step_halo(mm_ring *r, int step, const void *halo, int halo_frames, const void *in, void *out,
+                      void *hip_stream)
+{
+    if (!r || !in || !out || step < 0 || halo_frames < 0 || (halo_frames > 0 && !halo))
+        return MM_ERR_INVALID;
+    if (!r->halo_mode) {
+        snprintf(g_err, sizeof g_err, "mm_ring_step_halo is for IIR steerable handles");
+        return MM_ERR_UNSUPPORTED;
+    }
+    hipStream_t s = (hipStream_t)hip_stream;
+    HIP_TRY(hipSetDevice(r->device));
+    /* a filter started from rest at the halo's first frame (which passes
+     * through and seeds the local phases, as the stream's frame 0 does) */
+    int rc = mm_reset(r->h);
+    if (rc) return rc;
+    /* the halo's outputs are discarded: `out` holds them until the chunk
+     * overwrites it (at most `chunk` frames per call) */
+    const unsigned char *hp = (const unsigned char *)halo;
+    for (int f0 = 0; f0 < halo_frames; f0 += r->chunk) {
+        const int n = halo_frames - f0 < r->chunk ? halo_frames - f0 : r->chunk;
+        if ((rc = mm_process_stream(r->h, hp + r->frame_bytes * (size_t)f0, out, n, r->format, s))) return rc;
+    }
+    return mm_process_stream(r->h, in, out, r->chunk, r->format, s);
+}
+
+int mm_ring_halo_frames(const mm_ring *r, int *frames)
+{
+    if (!r || !frames) return MM_ERR_INVALID;
+    if (!r->halo_mode) {
+        *frames = 0;
+        return MM_OK;
+    }
+    mm_params p;
+    int rc = mm_get_params(r->h, &p);
+    if (rc) return rc;
+    /* the slower pole (1 - iir_low) decays below 1e-6 of its start value:
+     * ceil(ln 1e-6 / ln(1 - iir_low)); 270 frames at the default 0.05 */
+    const double d = 1.0 - (double)p.iir_low;
+    int k = 1;
+    double a = d;
+    while (a > 1e-6 && k < 100000) {
+        a *= d;
+        ++k;
+    }
+    *frames = k;
+    return MM_OK;
+}

@@ -75,7 +75,15 @@ typedef struct interop {
     uint64_t set_done[2];            /* timeline value that ends the set's last use */
     hipStream_t stream;
     PFN_vkWaitSemaphores wait_sem;
+    PFN_vkSignalSemaphore signal_sem;
+    int broken;                      /* a leg failed: later events return at once and
+                                        mm_unity_event_ok() tells C# to Blit instead */
 } interop;
+
+/* Host waits on the timeline are bounded: a chain that cannot complete (a
+ * device lost, a failed leg the repair below could not close) must not hang
+ * Unity's render thread. */
+#define MM_UNITY_WAIT_NS 2000000000ull
 
 static IUnityInterfaces *s_unity;
 static IUnityGraphics *s_graphics;
@@ -139,7 +147,8 @@ static int make_shared_semaphore(const UnityVulkanInstance *vi)
     hd.handle.fd = fd;
     if (hipImportExternalSemaphore(&s_io.hsem, &hd) != hipSuccess) return MM_ERR_HIP;
     s_io.wait_sem = (PFN_vkWaitSemaphores)vkGetDeviceProcAddr(vi->device, "vkWaitSemaphores");
-    return s_io.wait_sem ? MM_OK : MM_ERR_UNSUPPORTED;
+    s_io.signal_sem = (PFN_vkSignalSemaphore)vkGetDeviceProcAddr(vi->device, "vkSignalSemaphore");
+    return s_io.wait_sem && s_io.signal_sem ? MM_OK : MM_ERR_UNSUPPORTED;
 }
 
 static int make_command_buffers(const UnityVulkanInstance *vi)
@@ -240,10 +249,34 @@ static int submit(VkCommandBuffer cb, uint64_t wait, uint64_t signal)
     return vkQueueSubmit(s_io.queue, 1, &si, VK_NULL_HANDLE) == VK_SUCCESS;
 }
 
+static int host_wait(uint64_t value)
+{
+    VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &value};
+    return s_io.wait_sem(s_io.dev, &wi, MM_UNITY_WAIT_NS) == VK_SUCCESS;
+}
+
+static int host_signal(uint64_t value)
+{
+    VkSemaphoreSignalInfo si = {VK_STRUCTURE_TYPE_SEMAPHORE_SIGNAL_INFO, NULL, s_io.sem, value};
+    return s_io.signal_sem(s_io.dev, &si) == VK_SUCCESS;
+}
+
+/* A leg of frame i failed after X_i was submitted: bring the timeline to 3i+3
+ * from the host (after the legs that did queue have completed, since a
+ * timeline value only moves forward), so that nothing queued later waits
+ * forever, and stop using the interop (C# falls back to Graphics.Blit). */
+static void close_chain(uint64_t reached, uint64_t base)
+{
+    s_io.broken = 1;
+    if (reached > base && !host_wait(reached)) return;   /* device lost: nothing to close */
+    if (reached < base + 3) (void)host_signal(base + 3);
+    s_io.set_done[0] = s_io.set_done[1] = 0;
+}
+
 /* Render-thread callback: the three legs of the header comment. */
 static void UNITY_INTERFACE_API on_render_event(int event_id, void *data)
 {
-    if (event_id != MM_UNITY_EVENT_PROCESS || !s_vulkan || !data || !s_io.h) return;
+    if (event_id != MM_UNITY_EVENT_PROCESS || !s_vulkan || !data || !s_io.h || s_io.broken) return;
     const mm_unity_frame *f = (const mm_unity_frame *)data;
     /* current layouts, no barrier from Unity (the plugin's own command
      * buffers move and restore them) */
@@ -257,31 +290,55 @@ static void UNITY_INTERFACE_API on_render_event(int event_id, void *data)
     const uint64_t i = s_io.frame, base = 3 * i;
     const int set = (int)(i & 1);
     /* the set's command buffers were last submitted for frame i-2 */
-    if (s_io.set_done[set]) {
-        VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &s_io.set_done[set]};
-        if (s_io.wait_sem(s_io.dev, &wi, UINT64_MAX) != VK_SUCCESS) return;
+    if (s_io.set_done[set] && !host_wait(s_io.set_done[set])) {
+        s_io.broken = 1;
+        return;
     }
     if (!record_copy(s_io.cb[set][0], &src, s_io.buf[0], 1, f->width, f->height) ||
         !record_copy(s_io.cb[set][1], &dst, s_io.buf[1], 0, f->width, f->height))
-        return;
+        return;   /* nothing submitted: the timeline stays at 3i */
     /* X_i: source -> buf[0] after Y_{i-1} (value 3i) */
     if (!submit(s_io.cb[set][0], base, base + 1)) return;
     s_io.frame = i + 1;   /* from here on the chain must reach 3i+3 */
-    /* H_i: mm_process on the imported buffers, between 3i+1 and 3i+2 */
+    /* H_i: mm_process on the imported buffers, between 3i+1 and 3i+2.  If the
+     * stream cannot be made to wait for X_i, waiting on the host for it keeps
+     * mm_process from reading buf[0] early. */
     hipExternalSemaphoreWaitParams wp;
     memset(&wp, 0, sizeof wp);
     wp.params.fence.value = base + 1;
-    (void)hipWaitExternalSemaphoresAsync(&s_io.hsem, &wp, 1, s_io.stream);
+    if (hipWaitExternalSemaphoresAsync(&s_io.hsem, &wp, 1, s_io.stream) != hipSuccess && !host_wait(base + 1)) {
+        close_chain(base + 1, base);
+        return;
+    }
     void *in = mm_ext_frames_ptr(s_io.ext[0]), *out = mm_ext_frames_ptr(s_io.ext[1]);
-    if (mm_process(f->h, in, out, MM_RGBA8, MM_FRAMES_ON_DEVICE, s_io.stream) != MM_OK)
-        (void)hipMemcpyAsync(out, in, s_io.frame_bytes, hipMemcpyDeviceToDevice, s_io.stream);   /* .cs:105 */
+    if (mm_process(f->h, in, out, MM_RGBA8, MM_FRAMES_ON_DEVICE, s_io.stream) != MM_OK &&
+        hipMemcpyAsync(out, in, s_io.frame_bytes, hipMemcpyDeviceToDevice, s_io.stream) != hipSuccess) {   /* .cs:105 */
+        (void)hipStreamSynchronize(s_io.stream);
+        close_chain(base + 1, base);
+        return;
+    }
     hipExternalSemaphoreSignalParams sp;
     memset(&sp, 0, sizeof sp);
     sp.params.fence.value = base + 2;
-    (void)hipSignalExternalSemaphoresAsync(&s_io.hsem, &sp, 1, s_io.stream);
+    if (hipSignalExternalSemaphoresAsync(&s_io.hsem, &sp, 1, s_io.stream) != hipSuccess) {
+        /* H_i's work is queued but will not signal: finish it on the host */
+        (void)hipStreamSynchronize(s_io.stream);
+        close_chain(base + 1, base);
+        return;
+    }
     /* Y_i: buf[1] -> destination after H_i, in this same event */
-    (void)submit(s_io.cb[set][1], base + 2, base + 3);
+    if (!submit(s_io.cb[set][1], base + 2, base + 3)) {
+        close_chain(base + 2, base);
+        return;
+    }
     s_io.set_done[set] = base + 3;
+}
+
+/* For C#: false once the interop has failed (then OnRenderImage Blits source
+ * to destination itself, the reference's error path .cs:103-107). */
+UNITY_INTERFACE_EXPORT int UNITY_INTERFACE_API mm_unity_event_ok(void)
+{
+    return s_io.h && !s_io.broken;
 }
 
 UNITY_INTERFACE_EXPORT UnityRenderingEventAndData UNITY_INTERFACE_API mm_unity_event_func(void)
@@ -297,7 +354,7 @@ UNITY_INTERFACE_EXPORT void UNITY_INTERFACE_API mm_unity_destroy(mm_handle *h)
     if (s_io.frame && s_io.wait_sem) {
         const uint64_t last = 3 * s_io.frame;
         VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &last};
-        (void)s_io.wait_sem(s_io.dev, &wi, UINT64_MAX);
+        (void)s_io.wait_sem(s_io.dev, &wi, MM_UNITY_WAIT_NS);
     }
     if (s_io.stream) (void)hipStreamSynchronize(s_io.stream);
     for (int k = 0; k < 2; ++k)

@@ -8,7 +8,11 @@ gated stream, and requires that the entry point returns (it waited for A's own
 work only, never for the device: DESIGN.md §7b), that B's work was still held
 when it did, and that B's output after the release is intact.
 
-usage: python tests/gate_scenarios.py set_params|set_batch|destroy
+Two more scenarios hold handle A's OWN stream and require that mm_set_batch
+and mm_destroy of A wait for A's queued work before its buffers go back to
+the pool (own_set_batch, own_destroy).
+
+usage: python tests/gate_scenarios.py set_params|set_batch|destroy|own_set_batch|own_destroy
 """
 import ctypes
 import os
@@ -149,6 +153,88 @@ def destroy():
     check("mm_destroy", *returns_while_other_stream_gated(a.close))
 
 
+def _own_gated(a, sa, queue_work, op):
+    """Holds handle A's OWN stream sa behind a gate, queues A's work on it
+    (queue_work), runs op() (an entry point that frees or swaps buffers that
+    work reads) in a thread -> (op still blocked while A's work was held,
+    op returned after the release).  ADVICE r4: the stream-ordered frees
+    (hipFreeAsync behind last_ev) must not run ahead of A's queued kernels."""
+    import time
+    gate = Gate()
+    th = threading.Thread(target=op)
+    try:
+        gate.hold(sa.cuda_stream)
+        queue_work()
+        th.start()
+        time.sleep(1.0)
+        blocked = th.is_alive() and not sa.query()
+    finally:
+        gate.release()
+    th.join(20.0)
+    returned = not th.is_alive()
+    torch.cuda.synchronize()
+    gate.free()
+    return blocked, returned
+
+
+def own_set_batch():
+    """A's 8-frame 1080p stream is queued behind a gate on A's stream; a
+    concurrent mm_set_batch of A (which retires G and Q and moves the state
+    slot) must wait for that work, and A's outputs, including the frames after
+    the batch change, equal an ungated handle's."""
+    W, H = 1920, 1080
+    p = mm355.Params.make(phase_scale=25.0)
+    n = 8
+    frames = torch.empty((2 * n, H, W, 4), dtype=torch.uint8, device="cuda")
+    r = mm355.Handle(W, H, p)
+    r.set_batch(n)
+    r.synth(frames, 0, 2 * n)
+    ref = torch.empty_like(frames)
+    r.process_stream(frames, ref, 2 * n, mm355.RGBA8)
+    torch.cuda.synchronize()
+    a = mm355.Handle(W, H, p)
+    a.set_batch(n)
+    out = torch.zeros_like(frames)
+    sa = torch.cuda.Stream()
+    blocked, returned = _own_gated(
+        a, sa, lambda: a.process_stream(frames[:n], out[:n], n, mm355.RGBA8, stream=sa.cuda_stream),
+        lambda: a.set_batch(3))
+    assert blocked, "mm_set_batch returned while the handle's own work was still held"
+    assert returned, "mm_set_batch did not return after the release"
+    a.process_stream(frames[n:], out[n:], n, mm355.RGBA8, stream=sa.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), "A's output across a set_batch issued while its work was queued"
+    a.close()
+    r.close()
+
+
+def own_destroy():
+    """mm_destroy of A while A's own stream is held: it returns only after the
+    held work ran (the buffers it reads go back to the pool behind it), and
+    that work's output is complete."""
+    W, H = 1920, 1080
+    p = mm355.Params.make(phase_scale=25.0)
+    n = 8
+    frames = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    r = mm355.Handle(W, H, p)
+    r.set_batch(n)
+    r.synth(frames, 0, n)
+    ref = torch.empty_like(frames)
+    r.process_stream(frames, ref, n, mm355.RGBA8)
+    torch.cuda.synchronize()
+    a = mm355.Handle(W, H, p)
+    a.set_batch(n)
+    out = torch.zeros_like(frames)
+    sa = torch.cuda.Stream()
+    blocked, returned = _own_gated(
+        a, sa, lambda: a.process_stream(frames, out, n, mm355.RGBA8, stream=sa.cuda_stream), a.close)
+    assert blocked, "mm_destroy returned while the handle's own work was still held"
+    assert returned, "mm_destroy did not return after the release"
+    assert torch.equal(out, ref), "A's held work lost its buffers"
+    r.close()
+
+
 if __name__ == "__main__":
-    {"set_params": set_params, "set_batch": set_batch, "destroy": destroy}[sys.argv[1]]()
+    {"set_params": set_params, "set_batch": set_batch, "destroy": destroy,
+     "own_set_batch": own_set_batch, "own_destroy": own_destroy}[sys.argv[1]]()
     print(f"{sys.argv[1]}: ok")

@@ -49,3 +49,30 @@ def test_cpu_worker_runs_oracle(tmp_path):
     import numpy as np
     outs = np.load(out + ".npy")
     assert outs.shape == (3, 48, 64, 4) and outs.dtype == np.uint8
+
+
+def test_cpu_worker_boundary_pairs_equal_sequential(tmp_path):
+    """The boundary frames the bench's parity check adds (oracle reset, fed
+    frames t-1 and t) equal the sequential oracle's frame t: output t depends
+    only on inputs t-1 and t (.cs:142)."""
+    import numpy as np
+    out = str(tmp_path / "w.json")
+    subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-worker", "--cpu-out", out,
+                    "--cpu-threads", "2", "--cpu-frames", "5", "--cpu-seconds", "60",
+                    "--width", "64", "--height", "48", "--levels", "5", "--cpu-keep",
+                    "--cpu-pairs", "2,5"], check=True, timeout=120)
+    seq = np.load(out + ".npy")
+    pairs = np.load(out + ".pairs.npy")
+    assert np.array_equal(pairs[0], seq[2]) and np.array_equal(pairs[1], seq[5])
+
+
+def test_boundary_frames_cover_k2_launch_shapes():
+    """300 frames in batches of 150 at 1080p: each batch's prime, the packed
+    block's hand-off to k_cols_tail (40 %: frame 90 of a batch), the second-half
+    tails (10 %: frame 135) and the batch ends; frames 1..30 are sequential."""
+    b = bench.boundary_frames(300, 150, 1920, 1080)
+    for t in (89, 90, 134, 135, 149, 150, 151, 239, 240, 284, 285, 299):
+        assert t in b
+    assert all(31 <= t < 300 for t in b)
+    # 2160p: 30 % tails
+    assert 105 in bench.boundary_frames(300, 150, 3840, 2160)

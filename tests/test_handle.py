@@ -230,6 +230,19 @@ def test_destroy_does_not_stall_other_streams():
     _gate_scenario("destroy")
 
 
+def test_set_batch_waits_for_own_queued_work():
+    """mm_set_batch issued while the handle's own work is held on
+    its stream returns only after that work ran; outputs equal an ungated
+    handle's across the batch change (tests/gate_scenarios.py own_set_batch)."""
+    _gate_scenario("own_set_batch")
+
+
+def test_destroy_waits_for_own_queued_work():
+    """mm_destroy with the handle's own work held on its stream
+    frees the buffers only behind that work (own_destroy)."""
+    _gate_scenario("own_destroy")
+
+
 def test_steerable_set_state_then_pyramid_passes_through():
     """ADVICE r3: a steerable mm_set_state sets only the local-phase planes;
     after switching that handle to pyramid mode the G_{t-1} slot holds no
@@ -254,6 +267,32 @@ def test_steerable_set_state_then_pyramid_passes_through():
     ref = _stream(mm355.Handle(W, H, pp), dev, mm355.RGBA32F, [4])
     assert torch.equal(got[0], dev[0])
     assert torch.equal(got, ref)
+    # a handle that HAS run frames (its G slot holds an old frame)
+    # must not pair the next pyramid frame with that stale slot either
+    u = mm355.Handle(W, H, ps)
+    junk = _dev(T.synth(W, H, 3, seed=7))
+    _stream(u, junk, mm355.RGBA32F, [3])
+    u.set_state(st)
+    u.set_params(pp)
+    got = _stream(u, dev, mm355.RGBA32F, [4])
+    assert torch.equal(got[0], dev[0]), "first frame after a steerable set_state must pass through"
+    assert torch.equal(got, ref)
+    # the reverse: a pyramid set_state leaves no stale local-phase planes, so
+    # switching to steerable passes the next frame through as well
+    pst = torch.empty(mm355.Handle(W, H, pp).state_bytes, dtype=torch.uint8, device="cuda")
+    q = mm355.Handle(W, H, pp)
+    q.process_stream(dev[:2], torch.empty_like(dev[:2]), 2, mm355.RGBA32F)
+    q.get_state(pst)
+    v = mm355.Handle(W, H, ps)
+    _stream(v, junk, mm355.RGBA32F, [3])
+    v.set_params(pp)
+    v.set_state(pst)
+    v.set_params(ps)
+    gs = _stream(v, dev, mm355.RGBA32F, [4])
+    rs = _stream(mm355.Handle(W, H, ps), dev, mm355.RGBA32F, [4])
+    assert torch.equal(gs[0], dev[0]), "first steerable frame after a pyramid set_state must pass through"
+    assert torch.equal(gs, rs)
+    u.close(), v.close(), q.close()
     with pytest.raises(mm355.MMError):
         g = mm355.Handle(W, H, ps)
         g.set_state(st)

@@ -31,8 +31,8 @@ def header_symbols():
 
 def test_ring_library_exports_header_symbols():
     syms = header_symbols()
-    assert syms == ["mm_ring_create", "mm_ring_destroy", "mm_ring_get_id", "mm_ring_last_error",
-                    "mm_ring_step"]
+    assert syms == ["mm_ring_create", "mm_ring_destroy", "mm_ring_get_id", "mm_ring_halo_frames",
+                    "mm_ring_last_error", "mm_ring_step", "mm_ring_step_halo"]
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
                          check=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
@@ -151,3 +151,67 @@ def test_c_ring_local_c4_world8_2400_frames():
     assert len(a) == 2400 and a == b
     c = _checksums(_cli(common + ["-n", "720", "-b", "30", "--ring-local", "8"], 240))
     assert c == a[:720]
+
+
+# ---- round 5: every K2 / band-kernel instance through the ring ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,extra,world,batch,steps", [
+    # C3: 3840x2160, L = 6 (the two-band op at N = 4096), batches >= 24 so
+    # K2 runs its packed-block and second-half tails, world 3
+    ("c3_l6", ["-w", "3840", "-h", "2160", "-l", "6"], 3, 24, 2),
+    # standard mode (f1: its own K2 instance and prime), 1080p, world 2
+    ("standard", ["-w", "1920", "-h", "1080", "--standard"], 2, 24, 2),
+    # steerable O = 8 DIFF (f2: the state is the local-phase planes), world 2
+    ("steer_o8_diff", ["-w", "1920", "-h", "1080", "--orientations", "8"], 2, 8, 2),
+])
+def test_c_ring_local_instances_equal_single_stream(name, extra, world, batch, steps):
+    """The prime / in-loop bitwise invariant in every kernel instance the ring
+    can carry: rank threads on one GPU (local transport), per-frame FNV-1a
+    hashes of the sharded stream == one rank's stream (.cs:142: the only
+    temporal state)."""
+    n = world * batch * steps
+    common = extra + ["-n", str(n), "-b", str(batch), "-s", "25", "--checksum"]
+    a = _checksums(_cli(common, 240))
+    b = _checksums(_cli(common + ["--ring-local", str(world)], 300))
+    assert len(a) == n and a == b
+
+
+def _compare_summary(txt):
+    m = re.search(r"^compare frames (\d+) maxabs (\d+) ndiff (\d+) values (\d+)$", txt, flags=re.M)
+    assert m, txt[-2000:]
+    per = [(int(t), int(mx), int(nd)) for t, mx, nd in re.findall(r"^cmp (\d+) (\d+) (\d+)$", txt, flags=re.M)]
+    return tuple(int(x) for x in m.groups()), per
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,batch,steps", [(2, 300, 2), (3, 300, 1)])
+def test_c_ring_local_iir_halo_1080p_o8(world, batch, steps):
+    """the IIR steerable filter frame-sharded with a warm-up
+    halo (mm_ring_step_halo): each rank restarts its filter from rest
+    mm_ring_halo_frames() = 270 frames before its chunk (the slower pole
+    (1 - 0.05)^270 < 1e-6).  1080p, O = 8, chunks of 300 frames: the chunks
+    not starting within 270 frames of the stream's start differ from the
+    single-rank stream, within the RGBA8 parity bar (max 1 LSB on <= 0.1 % of
+    values); the first chunk (the stream's own start) is bitwise equal."""
+    n = world * batch * steps
+    out = _cli(["-w", "1920", "-h", "1080", "--orientations", "8", "--iir", "-n", str(n), "-b", str(batch),
+                "-s", "25", "--ring-local", str(world), "--compare"], 540)
+    (frames, mx, nd, values), per = _compare_summary(out)
+    assert frames == n and len(per) == n
+    assert mx <= 1 and nd <= 1e-3 * values, (mx, nd, values)
+    for t, fmx, fnd in per:
+        if t < batch:   # rank 0 of step 0: the stream's own start, no halo
+            assert fnd == 0, (t, fmx, fnd)
+
+
+def test_ring_step_refuses_iir_without_halo_cpu_args():
+    """mm_ring_step_halo validates its arguments before any device work."""
+    import ctypes
+    L = ctypes.CDLL(LIB)
+    L.mm_ring_step_halo.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    assert L.mm_ring_step_halo(None, 0, None, 0, None, None, None) == -1
+    L.mm_ring_halo_frames.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert L.mm_ring_halo_frames(None, None) == -1
