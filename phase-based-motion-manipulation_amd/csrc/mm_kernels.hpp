@@ -17,6 +17,7 @@
 #pragma once
 #include "mm_fft.hpp"
 #include <stdint.h>
+#include <type_traits>
 
 namespace mm {
 
@@ -1334,7 +1335,12 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
     // made opaque): an instance specialised on a constant fr = -1 computed an
     // F_{t-1} 1 ulp away from the in-loop one, which broke the bitwise
     // equality of one-frame calls, tails, ring hand-offs and batches.
-    auto frame_iter = [&](const int fr) __attribute__((always_inline)) -> bool {
+    // OPK: the regular groups' op, fixed per loop instance (the one-band op or
+    // the rest, chosen once per wave: wave_two_band is frame-invariant), so the
+    // register allocation of the one-band loop is not shaped by the generic
+    // op's live values; -1: chosen per frame at run time (block 0)
+    auto frame_iter = [&](const int fr, auto opk_c) __attribute__((always_inline)) -> bool {
+        constexpr int OPK = decltype(opk_c)::value;
         // Opaque per-iteration copy of the lane index: stops LICM from hoisting
         // every t-derived LDS address and twiddle of both FFTs out of the frame
         // loop (that pinned ~200 VGPRs and capped occupancy at 1 wave/SIMD).
@@ -1425,7 +1431,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             if (pass_frame) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) prev[j] = v[j];
-            } else if (k2_one_band_op<MODE>() && !wave_two_band) {
+            } else if (k2_one_band_op<MODE>() && (OPK == 1 || (OPK < 0 && !wave_two_band))) {
                 // no bin of this wave has two middle bands: branch-free op, bins
                 // interleaved MM_K2_OPG at a time
                 // bin j: fy = fy0 + j N/8 (fy0 = fft_bin(t, 0)), table entry fy
@@ -1665,13 +1671,30 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         K2_STAMP(6);
         return true;
     };
-    {
-        int fr_prime = -1;   // opaque: the prime instance keeps the runtime passthrough test
-        asm volatile("" : "+s"(fr_prime));
-        frame_iter(fr_prime);
-    }
-    for (int fr = 0;; ++fr)
-        if (!frame_iter(fr)) break;   // (fr >= 0 here: no passthrough branch)
+#ifndef MM_K2_UNROLL
+#define MM_K2_UNROLL 1
+#endif
+    auto run_frames = [&](auto opk_c) __attribute__((always_inline)) {
+        {
+            int fr_prime = -1;   // opaque: the prime instance keeps the runtime passthrough test
+            asm volatile("" : "+s"(fr_prime));
+            frame_iter(fr_prime, opk_c);
+        }
+#if MM_K2_UNROLL == 2
+        // two frames per trip: F_{t-1} alternates between the two bodies'
+        // registers instead of being copied back at the loop's end
+        for (int fr = 0;; fr += 2) {
+            if (!frame_iter(fr, opk_c)) break;
+            if (!frame_iter(fr + 1, opk_c)) break;
+        }
+#else
+        for (int fr = 0;; ++fr)
+            if (!frame_iter(fr, opk_c)) break;   // (fr >= 0 here: no passthrough branch)
+#endif
+    };
+    if constexpr (blk0 || !k2_one_band_op<MODE>()) run_frames(std::integral_constant<int, -1>());
+    else if (!wave_two_band) run_frames(std::integral_constant<int, 1>());
+    else run_frames(std::integral_constant<int, 0>());
 #ifdef MM_K2_STAMPS
     st_acc[7] = (__builtin_amdgcn_s_memrealtime() - st_acc[7]) << 32 | (st_acc[7] & 0xffffffffull);
     __builtin_amdgcn_s_waitcnt(0);   // every load and store of the wave completed

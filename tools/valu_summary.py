@@ -4,9 +4,13 @@
 usage: valu_summary.py PMC_DIR[,PMC_DIR...] KERNEL_TRACE_DIR OUT_JSON [CONFIG]
 
 valu_busy = SQ_INSTS_VALU * 4 cycles / (SIMDs * kernel cycles), with the
-kernel's cycles from its average kernel-trace duration and the shader clock
-derived from SQ_BUSY_CYCLES (summed over the shader engines) over that
-duration.  4 cycles = issue cost of one wave64 VALU instruction on gfx950,
+kernel's cycles from its AVERAGE kernel-trace duration over the launches of
+the largest grid (the ones the counters are quoted for; round 4 took the
+maximum duration, which one slow launch inflates: VERDICT r4 weak #2) and
+the shader clock derived from SQ_BUSY_CYCLES (summed over the shader
+engines, averaged over the same-size launches of the PMC run) over that
+duration.  issue_floor_s = SQ_INSTS_VALU * 4 / (SIMDs * clock): the time the
+launch's VALU instructions alone take at the clock it runs at.  4 cycles = issue cost of one wave64 VALU instruction on gfx950,
 MEASURED by tools/valu_calib.hip (profiles/r02_valu_calib.json: v_fma_f32
 4.17, v_add_f32 4.29, v_pk_fma_f32 4.18 cycles per wave-instruction per SIMD at
 8 waves/SIMD, clock from s_memtime/s_memrealtime; v_sin_f32 8.2).  A 2-cycle
@@ -31,30 +35,44 @@ def short(name):
     return m.group(1) if m else None
 
 
-pmc = defaultdict(lambda: defaultdict(list))
+# per kernel: grid size -> counter -> values (one per launch of that grid)
+pmc = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
 for f in [f for d in sys.argv[1].split(",") for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True)]:
     for r in csv.DictReader(open(f)):
         k = short(r["Kernel_Name"])
         if k:
-            pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-dur = defaultdict(list)
+            pmc[k][int(r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+dur = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(sys.argv[2] + "/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = short(r["Kernel_Name"])
         if k:
-            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+            grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+            dur[k][grid].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+
+
+def mean(v):
+    return sum(v) / len(v) if v else 0.0
+
+
 out = {}
-for k, c in pmc.items():
-    if k not in dur or "SQ_INSTS_VALU" not in c:
+for k, by_grid in pmc.items():
+    if k not in dur:
         continue
-    # launches differ in size (chunks); use the largest-launch averages
-    valu = max(c["SQ_INSTS_VALU"])
-    busy = max(c.get("SQ_BUSY_CYCLES", [0]))
-    t = max(dur[k])
+    # launches differ in size (chunks, tails): the largest grid both runs saw
+    grids = sorted(set(by_grid) & set(dur[k]))
+    if not grids or "SQ_INSTS_VALU" not in by_grid[grids[-1]]:
+        continue
+    c, ds = by_grid[grids[-1]], dur[k][grids[-1]]
+    valu = mean(c["SQ_INSTS_VALU"])
+    busy = mean(c.get("SQ_BUSY_CYCLES", []))
+    t = mean(ds)
     clk = busy / SES / t if busy else 2.0e9
-    out[k] = {"valu_insts_per_launch": valu, "salu_insts_per_launch": max(c.get("SQ_INSTS_SALU", [0])),
-              "lds_insts_per_launch": max(c.get("SQ_INSTS_LDS", [0])),
-              "launch_s": t, "clock_GHz": round(clk / 1e9, 3),
+    out[k] = {"valu_insts_per_launch": valu, "salu_insts_per_launch": mean(c.get("SQ_INSTS_SALU", [])),
+              "lds_insts_per_launch": mean(c.get("SQ_INSTS_LDS", [])),
+              "grid": grids[-1], "launches_timed": len(ds),
+              "launch_s": t, "launch_s_max": max(ds), "clock_GHz": round(clk / 1e9, 3),
+              "issue_floor_s": valu * 4 / (SIMDS * clk),
               "valu_busy": round(valu * 4 / (SIMDS * clk * t), 3),
               "valu_busy_peak_clk": round(valu * 4 / (SIMDS * 2.4e9 * t), 3)}
 if len(sys.argv) > 4:
