@@ -55,6 +55,7 @@ struct mm_handle {
     float *d_sst;               // temporal-filter state: phi, u_h, u_l planes [nb][Hn][W+4]
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
+    int sb_nf;                  // frames per k_sb_rows launch (MM_SB_NF; 2: pairs)
     bool steer_valid;           // d_sst holds the state after the previous frame
     // G: chunk + 1 slots of K1's row spectra.  Slot gs holds G_{t-1}, the row
     // spectra of the previous input frame: the temporal state
@@ -731,7 +732,8 @@ static int steer_alloc(mm_handle *h, hipStream_t s)
     h->d_sst = nullptr;
     h->steer_nb = -1;
     h->steer_valid = false;
-    if (h_alloc(h, &h->d_T, sizeof(c2) * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
+    // band rows of two frames (k_sb_rows runs frames in pairs)
+    if (h_alloc(h, &h->d_T, sizeof(c2) * 2 * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
         h_alloc(h, &h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
@@ -769,28 +771,40 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     // DIFF reads and writes only the phi plane (a caller's DIFF state buffer
     // holds just that plane); IIR the three
     const size_t plane = steer_planes(h) == 3 ? steer_plane_floats(h) : 0;
-    for (int k = 0; k < n; ++k) {
+    // frames in pairs: both frames' band columns, then one k_sb_rows launch
+    // whose workgroups carry the first frame's new state to the second in
+    // registers (MM_SB_NF=1: one frame per launch)
+    const size_t t_stride = band_stride * (size_t)(steer_bands(h) + 1);
+    for (int k = 0; k < n;) {
+        const int nf = (h->sb_nf >= 2 && k + 1 < n) ? 2 : 1;
         const int reset = k < seed;
-        {
+        for (int f = 0; f < nf; ++f) {
             ProfScope ps(h, s, MM_K_COLS, 0);
             const int g2 = sb_groups<LOG2N>();
             hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),
-                               sizeof(c2) * (size_t)g2 * lds_complex<N>(), s, h->d_Fb + fstride * k,
-                               h->d_T, band_stride, h->geo, h->spec, h->d_tw);
+                               sizeof(c2) * (size_t)g2 * lds_complex<N>(), s, h->d_Fb + fstride * (k + f),
+                               h->d_T + t_stride * f, band_stride, h->geo, h->spec, h->d_tw);
             HIPCHK(hipGetLastError());
         }
-        ProfScope ps(h, s, MM_K_ROWS_INV, reset || !write ? 0 : 1);
-        if (h->spec.filt == MM_FILTER_IIR)
-            hipLaunchKernelGGL((k_sb_rows<LOG2N, true>), dim3((h->geo.Hn + gpw - 1) / gpw),
-                               dim3(wg_threads<LOG2N>()), lds, s, h->d_T, band_stride,
-                               h->d_Yh + h->yh_stride * k, sst, sst + plane, sst + 2 * plane, reset,
-                               write && !reset ? 1 : 0, h->geo, h->spec, h->blur, h->d_tw);
-        else
-            hipLaunchKernelGGL((k_sb_rows<LOG2N, false>), dim3((h->geo.Hn + gpw - 1) / gpw),
-                               dim3(wg_threads<LOG2N>()), lds, s, h->d_T, band_stride,
-                               h->d_Yh + h->yh_stride * k, sst, sst + plane, sst + 2 * plane, reset,
-                               write && !reset ? 1 : 0, h->geo, h->spec, h->blur, h->d_tw);
+        // bit f: frame k + f's Yh (the stream's first frame passes through)
+        const int wmask = write ? ((reset ? 0 : 1) | (nf == 2 ? 2 : 0)) : 0;
+        ProfScope ps(h, s, MM_K_ROWS_INV, __builtin_popcount(wmask));
+        const dim3 grid((h->geo.Hn + gpw - 1) / gpw), block(wg_threads<LOG2N>());
+        float *yh = h->d_Yh + h->yh_stride * k;
+#define MM_SB_ROWS(IIRV, NFV)                                                                              \
+        hipLaunchKernelGGL((k_sb_rows<LOG2N, IIRV, NFV>), grid, block, lds, s, h->d_T, band_stride, t_stride, \
+                           yh, h->yh_stride, sst, sst + plane, sst + 2 * plane, reset, wmask, h->geo, h->spec, \
+                           h->blur, h->d_tw)
+        if (h->spec.filt == MM_FILTER_IIR) {
+            if (nf == 2) MM_SB_ROWS(true, 2);
+            else MM_SB_ROWS(true, 1);
+        } else {
+            if (nf == 2) MM_SB_ROWS(false, 2);
+            else MM_SB_ROWS(false, 1);
+        }
+#undef MM_SB_ROWS
         HIPCHK(hipGetLastError());
+        k += nf;
     }
     if (sst == h->d_sst) h->steer_valid = true;
     const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
@@ -1223,6 +1237,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k2_tail2_pct = getenv("MM_K2_TAIL2") ? atoi(getenv("MM_K2_TAIL2")) : 10;
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
     h->k34_oneshot = getenv("MM_K34_ONESHOT") ? atoi(getenv("MM_K34_ONESHOT")) : 1;
+    h->sb_nf = getenv("MM_SB_NF") ? atoi(getenv("MM_SB_NF")) : 2;
 
     h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * g.Hg;

@@ -142,6 +142,17 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
         const float ir = flat ? 0.0f : 1.0f / fr[j];
         cx[j] = fxs * ir;
         sy[j] = fys * ir;
+        // O = 6, 8: sum_k max(0, cos(theta - 2 pi k / O))^4 = 3 O / 16 for every
+        // theta (cos^4 = 3/8 + cos 2x / 2 + cos 4x / 8, and the O equally spaced
+        // lobes cancel the harmonics 2 and 4 when O divides neither; the max(0, .)
+        // keeps exactly half of the sum, the lobes o and o + O/2 being opposite).
+        // The constant replaces the per-bin O-term sum (same value to fp32
+        // rounding; k_sb_cols -6 %, O = 8 DIFF +3 % same-call,
+        // profiles/r05f_sb_isum_ab.txt).  O = 4 keeps the sum (harmonic 4 stays).
+        if (sp.O > 4) {
+            isum[j] = flat ? -1.0f : 16.0f / (3.0f * (float)sp.O);
+            continue;
+        }
         float sum = 0.0f;
         for (int k = 0; k < sp.O; ++k) sum += pow4(fmaxf(0.0f, cx[j] * sp.ang_c[k] + sy[j] * sp.ang_s[k]));
         isum[j] = flat ? -1.0f : 1.0f / sum;
@@ -237,11 +248,20 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 // are 1,084 four-wave workgroups: at 4 waves per SIMD 1,024 of them run at
 // once and the last 60 make a second round of the whole row time; at 5 they
 // all fit one round.
-template <int LOG2N, bool IIR>
+// NF consecutive frames per launch (1 or 2): a workgroup runs band b of
+// frame 0, then band b of frame 1 against frame 0's new state still in
+// registers, and writes the state planes once per NF frames (the DIFF planes
+// are read and written once per pair instead of per frame: 200 -> 100 MB per
+// 1080p frame at O = 8).  The same expressions in the same order as NF = 1:
+// bitwise the per-frame outputs.  Frame f's band rows at Tb + f * t_stride,
+// its Yh at Yh + f * yh_stride; reset applies to frame 0 (the stream's first
+// frame: it seeds the state and passes through); write_mask bit f: frame f's
+// Yh is wanted.
+template <int LOG2N, bool IIR, int NF>
 __global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR ? 4 : 5)))
-void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
+void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restrict__ Yh, size_t yh_stride,
                float *st_phi, float *st_uh, float *st_ul,
-               int reset, int write_out, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
+               int reset, int write_mask, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
@@ -258,11 +278,11 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
     preload_twiddles<LOG2N>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
-    // row k of band b (contiguous) and its state: loaded one band ahead
+    // row k of band b of frame f (contiguous) and its state: loaded one row ahead
     c2 v[8];
     float pp[8], puh[8], pul[8];
-    auto load_row = [&](int b, int t) {
-        const c2 *row = Tb + (size_t)b * band_stride + (size_t)k * N;
+    auto load_row = [&](int f, int b, int t) {
+        const c2 *row = Tb + (size_t)f * t_stride + (size_t)b * band_stride + (size_t)k * N;
 #pragma unroll
         for (int j = 0; j < 8; ++j)   // band_col_zero columns were never written: 0
             v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp) ? mk(0.0f, 0.0f) : row[t + j * T];
@@ -284,101 +304,128 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, float *__restrict__ Yh,
     {
         int t = t0;
         asm volatile("" : "+v"(t));
-        load_row(0, t);
+        load_row(0, 0, t);
         load_state(0, t);
     }
-    float y[8];
+    float y[NF][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) y[j] = 0.0f;
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[f][j] = 0.0f;
     for (int b = 0; b <= nb; ++b) {
-        int t = t0;
-        asm volatile("" : "+v"(t));
-        c2 wt[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            wt[i] = wtw[i];
-            if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
-        }
-        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
-        if (b == nb) {   // residual: Hermitian, real output
+        for (int f = 0; f < NF; ++f) {
+            int t = t0;
+            asm volatile("" : "+v"(t));
+            c2 wt[16];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) y[j] += v[j].x;
-            break;
-        }
-        // this band's new state and amplified synthesis, in registers
-        float nph[8], nuh[8], nul[8];
-        // local phases two bins at a time (packed FP32, fast_atan2's values)
-        float phs[8];
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-            const c2 p2 = fast_atan2_x2(v[j].y, v[j].x, v[j + 1].y, v[j + 1].x);
-            phs[j] = p2.x;
-            phs[j + 1] = p2.y;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float ph = phs[j];
-            float P = 0.0f, uh = 0.0f, ul = 0.0f;
-            if (!reset) {
-                if (!iir) {
-                    P = wrap_pi(pp[j] - ph);              // prev - cur, as the reference
-                } else {
-                    const float d = wrap_pi(ph - pp[j]);
-                    uh = (1.0f - sp.r_high) * (puh[j] + d);
-                    ul = (1.0f - sp.r_low) * (pul[j] + d);
-                    P = ul - uh;
-                }
+            for (int i = 0; i < 16; ++i) {
+                wt[i] = wtw[i];
+                if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
             }
-            nph[j] = ph;
-            nuh[j] = uh;
-            nul[j] = ul;
-            c2 s2 = v[j];
-            if (write_out && v[j].x * v[j].x + v[j].y * v[j].y >= sp.tau2) {
-                const float rev = P * sp.S_rev;
-                s2 = mul_c(v[j], mk(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)));
+            fft_regs_w<LOG2N, +1>(v, t, lds, wt);
+            if (b == nb) {   // residual: Hermitian, real output
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[f][j] += v[j].x;
+                if (f + 1 < NF) load_row(f + 1, nb, t);
+                continue;
             }
-            const int xi = (t + j * T - xs + N) & (N - 1);
-            if (xi < Wc) y[j] += 2.0f * s2.x;
-        }
-        load_row(b + 1, t);
-        __builtin_amdgcn_sched_barrier(0);   // row loads of b+1 ahead of the stores of b
-        if (valid) {
-            const size_t rs = ((size_t)b * g.Hn + k) * Wc;
+            // this band's new state and amplified synthesis, in registers
+            const bool rst = f == 0 && reset;            // the stream's first frame
+            const bool wr = ((write_mask >> f) & 1) != 0;
+            float nph[8], nuh[8], nul[8];
+            // local phases two bins at a time (packed FP32, fast_atan2's values)
+            float phs[8];
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                const c2 p2 = fast_atan2_x2(v[j].y, v[j].x, v[j + 1].y, v[j + 1].x);
+                phs[j] = p2.x;
+                phs[j + 1] = p2.y;
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
+                const float ph = phs[j];
+                float P = 0.0f, uh = 0.0f, ul = 0.0f;
+                if (!rst) {
+                    if (!iir) {
+                        P = wrap_pi(pp[j] - ph);              // prev - cur, as the reference
+                    } else {
+                        const float d = wrap_pi(ph - pp[j]);
+                        uh = (1.0f - sp.r_high) * (puh[j] + d);
+                        ul = (1.0f - sp.r_low) * (pul[j] + d);
+                        P = ul - uh;
+                    }
+                }
+                nph[j] = ph;
+                nuh[j] = uh;
+                nul[j] = ul;
+                c2 s2 = v[j];
+                if (wr && v[j].x * v[j].x + v[j].y * v[j].y >= sp.tau2) {
+                    const float rev = P * sp.S_rev;
+                    s2 = mul_c(v[j], mk(__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)));
+                }
                 const int xi = (t + j * T - xs + N) & (N - 1);
-                if (xi < Wc) {
-                    st_phi[rs + xi] = nph[j];
+                if (xi < Wc) y[f][j] += 2.0f * s2.x;
+            }
+            if (f + 1 < NF) {
+                // the next frame's row of this band; its previous state is this
+                // frame's new one, still in registers
+                load_row(f + 1, b, t);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    pp[j] = nph[j];
                     if (iir) {
-                        st_uh[rs + xi] = nuh[j];
-                        st_ul[rs + xi] = nul[j];
+                        puh[j] = nuh[j];
+                        pul[j] = nul[j];
+                    }
+                }
+                continue;
+            }
+            load_row(0, b + 1, t);
+            __builtin_amdgcn_sched_barrier(0);   // row loads of b+1 ahead of the stores of b
+            if (valid) {
+                const size_t rs = ((size_t)b * g.Hn + k) * Wc;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int xi = (t + j * T - xs + N) & (N - 1);
+                    if (xi < Wc) {
+                        st_phi[rs + xi] = nph[j];
+                        if (iir) {
+                            st_uh[rs + xi] = nuh[j];
+                            st_ul[rs + xi] = nul[j];
+                        }
                     }
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
+            load_state(b + 1, t);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        load_state(b + 1, t);
     }
-    if (!write_out) return;
     // |y| (ConvertComplexMagToTex) then the horizontal half of ApplyAntiAliasing
     float *raw = reinterpret_cast<float *>(lds);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[j]);
-    __syncthreads();
-    if (!valid) return;
-    float *out = Yh + (size_t)k * g.W;
     const bool interior = g.x0 >= 2 && g.x0 + g.W + 2 <= N;
-    for (int X = t0; X < g.W; X += T) {
-        const int c = g.x0 + X;
-        float acc;
-        if (interior) {
-            acc = bw.w0 * raw[c] + bw.w1 * (raw[c - 1] + raw[c + 1]) + bw.w2 * (raw[c - 2] + raw[c + 2]);
-        } else {
-            acc = bw.w0 * raw[wrap_idx(c, N, g.edge)];
-            acc += bw.w1 * (raw[wrap_idx(c - 1, N, g.edge)] + raw[wrap_idx(c + 1, N, g.edge)]);
-            acc += bw.w2 * (raw[wrap_idx(c - 2, N, g.edge)] + raw[wrap_idx(c + 2, N, g.edge)]);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        if (!((write_mask >> f) & 1)) continue;   // uniform
+        if (f > 0) __syncthreads();               // the previous frame's blur reads are done
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[f][j]);
+        __syncthreads();
+        if (valid) {
+            float *out = Yh + (size_t)f * yh_stride + (size_t)k * g.W;
+            for (int X = t0; X < g.W; X += T) {
+                const int c = g.x0 + X;
+                float acc;
+                if (interior) {
+                    acc = bw.w0 * raw[c] + bw.w1 * (raw[c - 1] + raw[c + 1]) + bw.w2 * (raw[c - 2] + raw[c + 2]);
+                } else {
+                    acc = bw.w0 * raw[wrap_idx(c, N, g.edge)];
+                    acc += bw.w1 * (raw[wrap_idx(c - 1, N, g.edge)] + raw[wrap_idx(c + 1, N, g.edge)]);
+                    acc += bw.w2 * (raw[wrap_idx(c - 2, N, g.edge)] + raw[wrap_idx(c + 2, N, g.edge)]);
+                }
+                out[X] = acc;
+            }
         }
-        out[X] = acc;
     }
 }
 
