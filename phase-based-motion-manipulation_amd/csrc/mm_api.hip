@@ -56,6 +56,7 @@ struct mm_handle {
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
     int sb_nf;                  // frames per k_sb_rows launch (MM_SB_NF; 2: pairs)
+    bool sb_stg_own;            // k_sb_cols stages in its own LDS area where it fits (MM_SB_STG)
     bool steer_valid;           // d_sst holds the state after the previous frame
     // G: chunk + 1 slots of K1's row spectra.  Slot gs holds G_{t-1}, the row
     // spectra of the previous input frame: the temporal state
@@ -781,9 +782,13 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         for (int f = 0; f < nf; ++f) {
             ProfScope ps(h, s, MM_K_COLS, 0);
             const int g2 = sb_groups<LOG2N>();
+            // the staging [Hn][GPW] gets its own LDS area where two workgroups
+            // per CU still fit (1080p: 54 KB), else it aliases the exchange buffers
+            const size_t lx = sizeof(c2) * (size_t)g2 * lds_complex<N>(), ls = sizeof(c2) * (size_t)g2 * h->geo.Hn;
+            const int own = h->sb_stg_own && lx + ls <= 81920 ? 1 : 0;
             hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),
-                               sizeof(c2) * (size_t)g2 * lds_complex<N>(), s, h->d_Fb + fstride * (k + f),
-                               h->d_T + t_stride * f, band_stride, h->geo, h->spec, h->d_tw);
+                               lx + (own ? ls : 0), s, h->d_Fb + fstride * (k + f),
+                               h->d_T + t_stride * f, band_stride, h->geo, h->spec, h->d_tw, own);
             HIPCHK(hipGetLastError());
         }
         // bit f: frame k + f's Yh (the stream's first frame passes through)
@@ -1238,6 +1243,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k34_rows = getenv("MM_K34_ROWS") ? atoi(getenv("MM_K34_ROWS")) / 4 * 4 : -1;
     h->k34_oneshot = getenv("MM_K34_ONESHOT") ? atoi(getenv("MM_K34_ONESHOT")) : 1;
     h->sb_nf = getenv("MM_SB_NF") ? atoi(getenv("MM_SB_NF")) : 2;
+    h->sb_stg_own = getenv("MM_SB_STG") ? atoi(getenv("MM_SB_STG")) != 0 : true;
 
     h->chunk = default_batch(width, height, N);
     h->g_stride = (size_t)(N / 2 + 1) * g.Hg;

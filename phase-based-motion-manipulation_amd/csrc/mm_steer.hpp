@@ -100,12 +100,16 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
 // (a column-major T made those reads 8-B gathers: 16x L2->L1 traffic).  The
 // band loop issues no loads (twiddle bases hoisted), so its stores are never
 // waited for.
+#ifndef MM_SB_COLS_WL
+#define MM_SB_COLS_WL 1
+#endif
 template <int LOG2N>
 __global__ __launch_bounds__(sb_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_stride, Geo g, Spec sp,
-               const c2 *__restrict__ tw)
+               const c2 *__restrict__ tw, int stg_own)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = sb_groups<LOG2N>();
+    constexpr bool SB_WL = MM_SB_COLS_WL && fft_c_v(LOG2N) > 1;
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
     const int t0 = threadIdx.x % T;
@@ -129,9 +133,13 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     const float fxs = sfreq<N>(kx);
     c2 v0[8];
     float fr[8], cx[8], sy[8], isum[8];
+    // the inverse column transform is the wave-local fft_dit (one workgroup
+    // barrier instead of six at N = 2048): its input is in fft_bin order, so
+    // register j of lane t holds bin ky = fft_bin(t, j) (the F column is read
+    // once, in that order), and its output is in natural row order as before
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int ky = t0 + j * T;
+        const int ky = SB_WL ? fft_bin<LOG2N>(t0, j) : t0 + j * T;
         c2 a = Fc[mir ? (N - ky) & (N - 1) : ky];     // F(-f) = conj F(f) (real input)
         if (mir) a.y = -a.y;
         v0[j] = scale(a, sp.inv_nn);
@@ -160,11 +168,14 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     c2 wtw[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles<LOG2N>(wtw, t0, tw);
+    if constexpr (SB_WL) preload_twiddles_wl<LOG2N>(wtw, t0, tw);
+    else preload_twiddles<LOG2N>(wtw, t0, tw);
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
     const int kx0 = blk * GPW;
-    c2 *stg = lds_all;   // [Hn][GPW]
+    // staging [Hn][GPW]: its own LDS area after the exchange buffers when
+    // stg_own (the launch sized the LDS for it), else over them
+    c2 *stg = stg_own ? lds_all + GPW * lds_complex<N>() : lds_all;
     // Bands level-major (b = o nmid + i - 1 as before): the radial mask of a
     // level is evaluated once for its O/2 orientation bands, which then only
     // add the angular factor (the same expressions per band: bitwise the
@@ -181,7 +192,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             wt[q] = wtw[q];
-            if (tw_slot_used(LOG2N, q)) asm volatile("" : "+v"(wt[q]));
+            if (SB_WL ? tw_slot_used_wl(LOG2N, q) : tw_slot_used(LOG2N, q)) asm volatile("" : "+v"(wt[q]));
         }
         // workgroup-uniform: skip the band where all its columns are zero
         bool all_zero = true;
@@ -205,8 +216,13 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
             }
             v[j] = scale(v0[j], m);
         }
-        fft_regs_w<LOG2N, +1>(v, t, lds, wt);
-        // every group has passed the barrier after its last exchange read
+        if constexpr (SB_WL) {
+            fft_dit<LOG2N, +1>(v, t, lds, wt);
+            // staging over the exchange buffers: every wave past its reads first
+            if (!stg_own) __syncthreads();
+        } else {
+            fft_regs_w<LOG2N, +1>(v, t, lds, wt);   // ends with a barrier after its last exchange read
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
@@ -227,7 +243,9 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
                 if (kx0 + c < N) out[(size_t)k * N + kx0 + c] = stg[e];
             }
         }
-        __syncthreads();   // the next band's FFT rewrites the buffers
+        // the next band's FFT rewrites the buffers (an own staging area: the
+        // next band's staging writes follow its FFT's barrier)
+        if (!stg_own) __syncthreads();
     }
 }
 
