@@ -181,6 +181,10 @@ __device__ __forceinline__ void apply_twiddles_tt(c2 *u, const float4 *p)
 }
 
 constexpr int fft_passes_v(int log2n) { return log2n / 3 + (log2n % 3 ? 1 : 0); }
+// twiddle-base slots P*4 + q (preload_twiddles): 16 up to N = 4096 (4
+// passes), 20 at N = 8192 (5 passes); unused slots are constant (1, 0) and
+// compile away
+constexpr int kTwSlots = 20;
 template <int LOG2N> constexpr int fft_passes() { return fft_passes_v(LOG2N); }
 constexpr int pass_radix_v(int log2n, int p) { return (p < log2n / 3) ? 8 : (log2n % 3 == 2 ? 4 : 2); }
 template <int LOG2N, int P> constexpr int pass_radix() { return pass_radix_v(LOG2N, P); }
@@ -200,7 +204,7 @@ constexpr int tw_entries_v(int log2n) { return 1 << log2n; }
 // TWST: stride of the table actually passed (a W_{N*TWST} table serves a
 // length-N transform at indices times TWST).
 template <int LOG2N, int P = 1, int TWST = 1>
-__device__ __forceinline__ void preload_twiddles(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
+__device__ __forceinline__ void preload_twiddles(c2 (&wb)[kTwSlots], int t, const c2 *__restrict__ tw)
 {
     if constexpr (P < fft_passes<LOG2N>()) {
         constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
@@ -267,7 +271,7 @@ __device__ __forceinline__ void xsync()
 // TT: the pass's twiddle powers come from the LDS table tt (tw_tab_build)
 // instead of products of the base wb[P*4 + q]
 template <int LOG2N, int P, int DIR, bool WSYNC = false, bool TT = false>
-__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+__device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[kTwSlots],
                                          const float4 *tt = nullptr)
 {
     constexpr int N = 1 << LOG2N, T = N / 8, R = pass_radix<LOG2N, P>(), B = 8 / R;
@@ -311,7 +315,7 @@ __device__ __forceinline__ void fft_pass(c2 (&v)[8], int t, c2 *lds, const c2 (&
 }
 
 template <int LOG2N, int DIR, int P, bool WSYNC = false, bool TT = false>
-__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+__device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[kTwSlots],
                                               const float4 *tt = nullptr)
 {
     if constexpr (P < fft_passes<LOG2N>()) {
@@ -326,7 +330,7 @@ __device__ __forceinline__ void fft_pass_loop(c2 (&v)[8], int t, c2 *lds, const 
 template <int LOG2N, int DIR>
 __device__ __forceinline__ void fft_regs(c2 (&v)[8], int t, c2 *lds, const c2 *__restrict__ tw)
 {
-    c2 wb[16];
+    c2 wb[kTwSlots];
     preload_twiddles<LOG2N>(wb, t, tw);
     fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wb);
 }
@@ -340,7 +344,7 @@ constexpr bool tw_slot_used(int log2n, int i)
 // Same, with the (forward) twiddle bases already in registers
 // (preload_twiddles): for loops that must not issue loads between frames.
 template <int LOG2N, int DIR>
-__device__ __forceinline__ void fft_regs_w(c2 (&v)[8], int t, c2 *lds, const c2 (&wf)[16])
+__device__ __forceinline__ void fft_regs_w(c2 (&v)[8], int t, c2 *lds, const c2 (&wf)[kTwSlots])
 {
     fft_pass_loop<LOG2N, DIR, 0>(v, t, lds, wf);
 }
@@ -363,7 +367,10 @@ __device__ __forceinline__ void fft_regs_w(c2 (&v)[8], int t, c2 *lds, const c2 
 // region w is wave w's for the inner transform.  On return from either, other
 // waves may still use their regions: __syncthreads() before any use of the
 // group's LDS by another wave.
-constexpr int fft_c_v(int log2n) { return log2n >= 9 ? 1 << (log2n - 9) : 1; }
+// C waves per transform for 1024 <= N <= 4096; N = 8192 (T = 1024 threads,
+// 16 waves: more than a thread's 8 values for the outer stage) runs the
+// all-workgroup Stockham transform in natural order, as C = 1
+constexpr int fft_c_v(int log2n) { return log2n >= 9 && log2n <= 12 ? 1 << (log2n - 9) : 1; }
 constexpr int fft_inner_v(int log2n) { return log2n >= 9 ? 9 : log2n; }
 constexpr int fft_region_v(int log2n) { return (1 << fft_inner_v(log2n)) + (1 << fft_inner_v(log2n)) / 8; }
 
@@ -412,7 +419,7 @@ template <int LOG2N> constexpr int zslot_h_size()
 // (slots 4, 8, from the W_N table at stride C) and, for C > 1, the outer
 // stage's W_N^{n2} for the thread's H values n2 (slots 12 + h).
 template <int LOG2N>
-__device__ __forceinline__ void preload_twiddles_wl(c2 (&wb)[16], int t, const c2 *__restrict__ tw)
+__device__ __forceinline__ void preload_twiddles_wl(c2 (&wb)[kTwSlots], int t, const c2 *__restrict__ tw)
 {
     constexpr int C = fft_c_v(LOG2N);
     if constexpr (C == 1) {
@@ -433,12 +440,12 @@ __device__ __forceinline__ void dft_c(c2 *u)
 }
 
 template <int LOG2N, int DIR, bool TT = false>
-__device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+__device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[kTwSlots],
                                         const float4 *tt = nullptr)
 {
     constexpr int C = fft_c_v(LOG2N), H = 8 / C, RS = fft_region_v(LOG2N);
-    if constexpr (C == 1) {
-        fft_pass_loop<LOG2N, DIR, 0, true>(v, t, lds, wb);
+    if constexpr (C == 1) {   // one wave per transform (N <= 512), or the whole workgroup (N = 8192)
+        fft_pass_loop<LOG2N, DIR, 0, ((1 << LOG2N) / 8 <= 64)>(v, t, lds, wb);
     } else {
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -462,12 +469,12 @@ __device__ __forceinline__ void fft_dif(c2 (&v)[8], int t, c2 *lds, const c2 (&w
 }
 
 template <int LOG2N, int DIR, bool TT = false>
-__device__ __forceinline__ void fft_dit(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[16],
+__device__ __forceinline__ void fft_dit(c2 (&v)[8], int t, c2 *lds, const c2 (&wb)[kTwSlots],
                                         const float4 *tt = nullptr)
 {
     constexpr int C = fft_c_v(LOG2N), H = 8 / C, RS = fft_region_v(LOG2N);
-    if constexpr (C == 1) {
-        fft_pass_loop<LOG2N, DIR, 0, true>(v, t, lds, wb);
+    if constexpr (C == 1) {   // one wave per transform (N <= 512), or the whole workgroup (N = 8192)
+        fft_pass_loop<LOG2N, DIR, 0, ((1 << LOG2N) / 8 <= 64)>(v, t, lds, wb);
     } else {
         const int w = t >> 6, l = t & 63;
         c2 *reg = lds + w * RS;

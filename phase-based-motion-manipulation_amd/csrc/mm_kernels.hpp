@@ -340,7 +340,7 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
     // column taps and twiddles with the pixel loads instead of one dependent
     // round trip each after them (batch launches: K1 +5 %, registers held
     // across the loads)
-    c2 wb[16];
+    c2 wb[kTwSlots];
     float4 cw[8];
     if constexpr (LAT && !GEN) {
         preload_twiddles_wl<LOG2N>(wb, t, tw);
@@ -1035,7 +1035,7 @@ __device__ __forceinline__ c2 k2_op(c2 c, c2 p, int fx, int fy, const Spec &sp, 
 #endif
 template <int LOG2N> constexpr int k2_groups()
 {
-    return LOG2N >= 12 ? MM_K2_GROUPS_4K : groups_at_least<LOG2N, MM_K2_GROUPS>();
+    return LOG2N >= 13 ? 1 : LOG2N >= 12 ? MM_K2_GROUPS_4K : groups_at_least<LOG2N, MM_K2_GROUPS>();
 }
 // the steerable band-column kernel: two columns per workgroup at every N
 template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, 2>(); }
@@ -1222,9 +1222,9 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #endif
     // twiddle bases of both FFTs, loaded once (issued under the table copy): no loads inside a frame but G's
     constexpr bool TT = k2_twtab<LOG2N>();
-    c2 wtw[16];
+    c2 wtw[kTwSlots];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    for (int i = 0; i < kTwSlots; ++i) wtw[i] = mk(1.0f, 0.0f);
     if constexpr (TT) {   // outer-stage bases only; the inner passes read ttab
 #pragma unroll
         for (int h = 0; h < 8 / fft_c_v(LOG2N); ++h) wtw[12 + h] = tw[t0 + 64 * fft_c_v(LOG2N) * h];
@@ -1414,9 +1414,9 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
             v[j] = packed ? mk(ga[j].x, gb[j]) : ga[j];
         // opaque per-iteration copy of the twiddle bases (same reason as t: the
         // products of their powers must not be hoisted into live registers)
-        c2 wt[16];
+        c2 wt[kTwSlots];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < kTwSlots; ++i) {
             wt[i] = wtw[i];
             if (tw_slot_used_wl(LOG2N, i) && !(TT && i < 12)) asm volatile("" : "+v"(wt[i]));
         }
@@ -2527,7 +2527,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
     return z ^ (z >> 31);
 }
 
-__global__ void k_synth(uint8_t *out, int W, int H, int t0, int count, uint64_t seed, int gray)
+static __global__ void k_synth(uint8_t *out, int W, int H, int t0, int count, uint64_t seed, int gray)
 {
     const size_t npx = (size_t)W * H;
     const size_t total = npx * count;

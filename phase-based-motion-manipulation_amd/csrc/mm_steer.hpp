@@ -165,9 +165,9 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
         for (int k = 0; k < sp.O; ++k) sum += pow4(fmaxf(0.0f, cx[j] * sp.ang_c[k] + sy[j] * sp.ang_s[k]));
         isum[j] = flat ? -1.0f : 1.0f / sum;
     }
-    c2 wtw[16];
+    c2 wtw[kTwSlots];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    for (int i = 0; i < kTwSlots; ++i) wtw[i] = mk(1.0f, 0.0f);
     if constexpr (SB_WL) preload_twiddles_wl<LOG2N>(wtw, t0, tw);
     else preload_twiddles<LOG2N>(wtw, t0, tw);
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
@@ -188,9 +188,9 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
         // hoisting the FFT addressing and twiddle powers into live registers
         int t = t0;
         asm volatile("" : "+v"(t));
-        c2 wt[16];
+        c2 wt[kTwSlots];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
+        for (int q = 0; q < kTwSlots; ++q) {
             wt[q] = wtw[q];
             if (SB_WL ? tw_slot_used_wl(LOG2N, q) : tw_slot_used(LOG2N, q)) asm volatile("" : "+v"(wt[q]));
         }
@@ -292,9 +292,9 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
     constexpr bool iir = IIR;
-    c2 wtw[16];
+    c2 wtw[kTwSlots];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) wtw[i] = mk(1.0f, 0.0f);
+    for (int i = 0; i < kTwSlots; ++i) wtw[i] = mk(1.0f, 0.0f);
     preload_twiddles<LOG2N>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
     // row k of band b of frame f (contiguous) and its state: loaded one row ahead
     c2 v[8];
@@ -335,9 +335,9 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
         for (int f = 0; f < NF; ++f) {
             int t = t0;
             asm volatile("" : "+v"(t));
-            c2 wt[16];
+            c2 wt[kTwSlots];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < kTwSlots; ++i) {
                 wt[i] = wtw[i];
                 if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
             }

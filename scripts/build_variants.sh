@@ -1,10 +1,20 @@
 # Build library variants: build_variants.sh name1 "FLAGS1" name2 "FLAGS2" ...
+# (every translation unit of csrc/ with the flags; -DMM_ONLY_LOG2N=L builds
+# mm_api.hip alone for one padded size)
 set -e
 cd /root/repo/phase-based-motion-manipulation_amd
-rm -rf lib/variants; mkdir -p lib/variants
+mkdir -p lib/variants
 while [ $# -gt 0 ]; do
   n=$1; f=$2; shift 2
-  /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result $f -shared -o lib/variants/$n.so csrc/mm_api.hip &
+  (
+    o=/tmp/variant_$n; rm -rf $o; mkdir -p $o
+    if echo "$f" | grep -q MM_ONLY_LOG2N; then srcs=csrc/mm_api.hip; else srcs=$(ls csrc/*.hip); fi
+    for s in $srcs; do
+      /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function $f -c -o $o/$(basename $s .hip).o $s &
+    done
+    wait
+    /opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 -shared -o lib/variants/$n.so $o/*.o
+  ) &
 done
 wait
 ls -la lib/variants

@@ -40,8 +40,9 @@ def test_create_rejects_bad_arguments_without_gpu():
     L = mm355.lib()
     st = mm355.Params.make(mode=mm355.MODE_STEERABLE, orientations=8)
     assert L.mm_create(63, 48, ctypes.byref(st), 0, ctypes.byref(h)) == -2  # odd width: steerable only
-    assert L.mm_create(8192, 48, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N > 4096
-    assert L.mm_create(4097, 2160, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N = 8192 (5K)
+    assert L.mm_create(8193, 48, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N > 8192
+    assert L.mm_create(5120, 48, ctypes.byref(st), 0, ctypes.byref(h)) == -2  # steerable: N <= 4096
+    assert L.mm_create(16385, 2160, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N = 32768
     assert L.mm_create(8, 6, ctypes.byref(p), 0, ctypes.byref(h)) == -2      # N = 8 < 16
     assert L.mm_create(2, 2, ctypes.byref(p), 0, ctypes.byref(h)) == -2      # N = 2
     assert not h.value                                                       # nothing created
@@ -110,7 +111,7 @@ def test_unity_shim_calls_only_declared_entry_points():
     src = open(os.path.join(os.path.dirname(mm355.LIB_PATH), "..", "unity", "mm_unity_plugin.c")).read()
     body = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     called = set(re.findall(r"\b(mm_[a-z_0-9]+)\s*\(", body))
-    own = {"mm_unity_create", "mm_unity_event_func", "mm_unity_destroy"}
+    own = {"mm_unity_create", "mm_unity_event_func", "mm_unity_event_ok", "mm_unity_destroy"}
     declared = set(mm355.abi_symbols())
     assert own <= called
     assert called - own <= declared, called - own - declared

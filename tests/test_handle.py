@@ -316,13 +316,20 @@ def test_smallest_canvas_n16(W, H, L, S, edge):
 
 
 def test_refused_geometries():
-    """max(W, H) <= 8 (N <= 8) and N = 8192 are refused with
-    MM_ERR_UNSUPPORTED, not computed on another canvas."""
+    """max(W, H) <= 8 (N <= 8) and max(W, H) > 8192 (N = 16384) are refused
+    with MM_ERR_UNSUPPORTED, not computed on another canvas; N = 8192 (5K/8K
+    screens, since round 5) is accepted except by the steerable extension."""
     import mm355
-    for W, H in ((8, 6), (4, 4), (2, 8), (4097, 2160), (8192, 4320)):
+    for W, H in ((8, 6), (4, 4), (2, 8), (8193, 2160), (16384, 8640)):
         with pytest.raises(mm355.MMError) as ei:
             mm355.Handle(W, H)
         assert ei.value.code == -2, (W, H)
+    h = mm355.Handle(5120, 2880)
+    assert h.N == 8192
+    h.close()
+    with pytest.raises(mm355.MMError) as ei:
+        mm355.Handle(5120, 2880, mm355.Params.make(mode=mm355.MODE_STEERABLE, orientations=8))
+    assert ei.value.code == -2
 
 
 @pytest.mark.parametrize("W,H,n", [(1920, 1080, 30), (640, 360, 48)])

@@ -120,3 +120,37 @@ def test_bench_launch_shape_vs_oracle():
         pair = [O.synth_frame(W, H, t - 1), O.synth_frame(W, H, t)]
         ref = _oracle_at(W, H, pair, 1, levels=5, phase_scale=25.0)
         T.assert_close_u8(out[t].cpu().numpy(), ref)
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_5k_n8192_vs_oracle():
+    """A 5K screen (5120x2880: N = NextPowerOfTwo(5120) = 8192, .cs:298-302),
+    refused before round 5: RGBA8 frame calls and one stream call against the
+    oracle (L = 5, S = 25), and the two call patterns bitwise equal."""
+    W, H, n = 5120, 2880, 3
+    O.set_threads(16)
+    fr = T.synth(W, H, n, fmt="u8")
+    ref = T.oracle_run(W, H, fr, 5, 25.0)
+    a = T.gpu_run(W, H, fr, 5, 25.0, mode="frame", batch=1)
+    b = T.gpu_run(W, H, fr, 5, 25.0, mode="stream", batch=3)
+    assert np.array_equal(a[0], fr[0])
+    for k in range(1, n):
+        assert np.array_equal(a[k], b[k])
+        T.assert_close_u8(a[k], ref[k])
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("W,H,L,S", [(4100, 48, 5, 9.7), (4200, 100, 6, 25.0)])
+def test_n8192_f32_vs_oracle(W, H, L, S):
+    """N = 8192 at the fp32 bar (wide, short canvases: every kernel's 8192-point
+    transform; L = 6: the two-band op), frame and stream calls."""
+    O.set_threads(16)
+    fr = T.synth(W, H, 3)
+    ref = T.oracle_run(W, H, fr, L, S)
+    for mode in ("frame", "stream"):
+        got = T.gpu_run(W, H, fr, L, S, mode=mode, batch=2)
+        assert np.array_equal(got[0], fr[0])
+        for k in range(1, 3):
+            T.assert_close_f32(got[k], ref[k], integer_scale=float(S).is_integer())
