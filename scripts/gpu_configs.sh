@@ -9,4 +9,6 @@ run() {
 }
 run c2 && run c3_4k --width 3840 --height 2160 --levels 6 && run c2_std --standard && \
 run c2_o8diff --orientations 8 && run c2_o8iir --orientations 8 --temporal-filter iir && \
-run c2_o4 --orientations 4 && run c2_fps60 --frames-per-step 60 --steps 5
+run c2_o4 --orientations 4 && run c2_fps60 --frames-per-step 60 --steps 5 && \
+run c3_o8diff --width 3840 --height 2160 --levels 6 --orientations 8 --steps 2 --warmup 1 && \
+run c5k --width 5120 --height 2880 --frames-per-step 30 --batch 15 --steps 2 --warmup 1

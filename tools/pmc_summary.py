@@ -37,16 +37,27 @@ def short(name):
     return f"{m.group(1)}_{4 * int(m.group(3) or 1)}"
 
 
+def frames_of_launch(name):
+    """Frames one launch of a per-frame kernel covers: k_sb_rows<L, IIR, NF>
+    runs NF frames (round 5: pairs), the band-column kernel one."""
+    m = re.search(r"k_sb_rows<\d+, (?:true|false), (\d+)>", name)
+    return int(m.group(1)) if m else 1
+
+
 def read_counter(d, counter):
+    """Mean counter value per launch; for the per-frame kernels (PER_FRAME)
+    the mean per FRAME (each launch divided by the frames it covers)."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = defaultdict(list)
     for f in files:
         for row in csv.DictReader(open(f)):
             if row.get("Counter_Name") != counter:
                 continue
-            k = short(row.get("Kernel_Name", ""))
+            name = row.get("Kernel_Name", "")
+            k = short(name)
             if k:
-                vals[k].append(float(row["Counter_Value"]))
+                div = frames_of_launch(name) if k in PER_FRAME else 1
+                vals[k].append(float(row["Counter_Value"]) / div)
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
@@ -66,7 +77,7 @@ def main():
         fc, wc = fb * fcorr.get(rw, 1.0), wb * wcorr.get(ww, 1.0)
         kernels[k] = {"fetch_bytes_raw": fb, "write_bytes_raw": wb,
                       "fetch_bytes": fc, "write_bytes": wc,
-                      "hbm_bytes_per_launch": fc + wc,
+                      "hbm_bytes_per_launch": fc + wc,   # per frame for PER_FRAME kernels
                       "hbm_bytes_per_frame": (fc + wc) / (1 if k in PER_FRAME else fpl),
                       "read_width": rw, "write_width": ww}
     if "k_sb_cols" in kernels and "k_cols_fwd" in kernels:
