@@ -7,7 +7,7 @@ T=$(mktemp -d /tmp/rev.XXXXXX)
 git -C /root/repo archive $REV phase-based-motion-manipulation_amd/csrc include | tar -x -C $T
 mkdir -p /root/repo/phase-based-motion-manipulation_amd/lib/variants
 for s in $T/phase-based-motion-manipulation_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result \
+  /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -ffp-contract=on -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result \
     -Wno-unused-function -c -o ${s%.hip}.o $s &
 done
 wait

@@ -10,7 +10,7 @@ while [ $# -gt 0 ]; do
     o=/tmp/variant_$n; rm -rf $o; mkdir -p $o
     if echo "$f" | grep -q MM_ONLY_LOG2N; then srcs=csrc/mm_api.hip; else srcs=$(ls csrc/*.hip); fi
     for s in $srcs; do
-      /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function $f -c -o $o/$(basename $s .hip).o $s &
+      /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize -ffp-contract=on -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function $f -c -o $o/$(basename $s .hip).o $s &
     done
     wait
     /opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 -shared -o lib/variants/$n.so $o/*.o
