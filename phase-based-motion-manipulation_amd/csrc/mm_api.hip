@@ -281,7 +281,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     build_spec(*p, N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->k2_sp = k2_power_exponent(h->spec, h->N);
-    h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
+    h->k2_tab2 = h->k2_tab && bands_overlap(h->spec) && h->N <= 4096;   // (N = 8192: LDS, set_attrs)
     h->ktab_mode = -1;
     h->blur = build_blur();
     // packed-block frames in k_cols_tail: 40 % at N <= 2048 since the prime
@@ -376,7 +376,7 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     build_spec(*p, h->N, h->spec);
     h->k2_tab = bands_fit_table(h->spec) && !getenv("MM_K2_NOTAB");
     h->k2_sp = k2_power_exponent(h->spec, h->N);
-    h->k2_tab2 = h->k2_tab && bands_overlap(h->spec);
+    h->k2_tab2 = h->k2_tab && bands_overlap(h->spec) && h->N <= 4096;   // (N = 8192: LDS, set_attrs)
     h->ktab_mode = -1;
     if (edge_changed) return upload_tables(h);
     return MM_OK;

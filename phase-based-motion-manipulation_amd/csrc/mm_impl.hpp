@@ -436,9 +436,8 @@ static int set_attrs(int W)
         MM_SET_K2(MM_K2_PYR_TAB, 0);
         MM_SET_K2(MM_K2_PYR_TAB, 25);
         MM_SET_K2(MM_K2_PYR_TAB, 10);
-        MM_SET_K2(MM_K2_PYR_TAB2, 0);
-        MM_SET_K2(MM_K2_PYR_TAB2, 25);
-        MM_SET_K2(MM_K2_PYR_TAB2, 10);
+        // (no two-band instance: its mask-sum arrays would take K2 past 160 KB
+        // of LDS at N = 8192; overlapping bands run the generic op there)
 #undef MM_SET_K2
     }
     if constexpr (LOG2N == 11) {   // k_rows_inv_compose4: four 2048-point groups, 73.7 KB
