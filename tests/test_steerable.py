@@ -154,3 +154,43 @@ def test_gpu_chunked_and_state_handoff():
             d.close()
         for h in (a, b, c):
             h.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("filt", [0, 1])
+def test_gpu_frames_per_launch_bitwise(filt):
+    """k_sb_rows runs 1 or 2 frames per launch (MM_SB_NF, read at mm_create),
+    carrying the band state from the first to the second in registers: the
+    same expressions in the same order, so the outputs and the final state are
+    bitwise equal for both groupings, including a batch (7) that leaves a
+    single frame."""
+    import os
+    import mm355
+    import torch
+    W, H, n = 200, 120, 9
+    fr = frames(W, H, n)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    p = mm355.Params.make(levels=5, phase_scale=10.0, mode=mm355.MODE_STEERABLE,
+                          orientations=8, temporal_filter=filt)
+    res = {}
+    old = os.environ.get("MM_SB_NF")
+    try:
+        for nf in ("1", "2"):
+            os.environ["MM_SB_NF"] = nf
+            h = mm355.Handle(W, H, p)
+            h.set_batch(7)
+            out = torch.empty_like(dev)
+            h.process_stream(dev, out, n, mm355.RGBA32F)
+            st = torch.empty(h.state_bytes, dtype=torch.uint8, device="cuda")
+            h.get_state(st)
+            torch.cuda.synchronize()
+            res[nf] = (out.cpu(), st.cpu())
+            h.close()
+    finally:
+        if old is None:
+            os.environ.pop("MM_SB_NF", None)
+        else:
+            os.environ["MM_SB_NF"] = old
+    for nf in ("2",):
+        assert torch.equal(res[nf][0], res["1"][0]), nf
+        assert torch.equal(res[nf][1], res["1"][1]), nf
