@@ -21,10 +21,10 @@
  *     (alpha included) and becomes the temporal state (.cs:111-117); after
  *     that output alpha is 1 (CombineYIQChannels.shader:56).
  *   - Geometry: the padded square is N = nextpow2(max(W, H)) (.cs:298-302);
- *     this build covers 16 <= N <= 4096, i.e. 9 <= max(W, H) <= 4096 (other
- *     sizes: MM_ERR_UNSUPPORTED from mm_create).  Odd W or H are supported in
- *     MM_MODE_PYRAMID and MM_MODE_STANDARD (and the debug views);
- *     MM_MODE_STEERABLE needs even W and H.  The fused K3+K4 kernel runs for
+ *     this build covers 16 <= N <= 8192, i.e. 9 <= max(W, H) <= 8192 (other
+ *     sizes: MM_ERR_UNSUPPORTED from mm_create); MM_MODE_STEERABLE stops at
+ *     N = 4096.  Odd W or H are supported in every mode (and the debug
+ *     views).  The fused K3+K4 kernel runs for
  *     even sizes with W % 8 == 0 and margins N - W >= 8, N - H >= 4; every
  *     other geometry takes the unfused pair (same results).
  *   - Every entry point that takes a handle runs on the handle's device and

@@ -228,9 +228,6 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     if (!out) return MM_ERR_INVALID;
     *out = nullptr;
     if (width < 2 || height < 2) return MM_ERR_UNSUPPORTED;
-    // odd sizes: the pyramid, standard and debug paths (the steerable extension's
-    // band kernels assume integer quad offsets)
-    if (((width | height) & 1) && p && p->mode == MM_MODE_STEERABLE) return MM_ERR_UNSUPPORTED;
     int rc = validate_params(p);
     if (rc) return rc;
     // N = Mathf.NextPowerOfTwo(max(W, H)) (.cs:298-302): the kernels' FFT

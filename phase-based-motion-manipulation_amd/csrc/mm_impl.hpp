@@ -739,7 +739,7 @@ static int steer_bands(const mm_handle *h)
 static int steer_planes(const mm_handle *h) { return h->spec.filt == MM_FILTER_IIR ? 3 : 1; }
 static size_t steer_plane_floats(const mm_handle *h)
 {
-    return (size_t)steer_bands(h) * h->geo.Hn * (h->W + 4);
+    return (size_t)steer_bands(h) * h->geo.Hn * (h->geo.Wy + 4);
 }
 static size_t steer_state_bytes(const mm_handle *h)
 {

@@ -75,7 +75,7 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
     const int logical = blockIdx.x * GPW + grp;
     const bool valid = logical < total_cols;
     const int fr = valid ? logical / F : 0, f = valid ? logical % F : 0;
-    const c2 *Gc = G + (size_t)fr * g_stride + (size_t)f * g.H;
+    const c2 *Gc = G + (size_t)fr * g_stride + (size_t)f * g.Hg;   // (H rows of Hg: K1 writes row pairs)
     c2 v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -288,7 +288,9 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
     const bool valid = logical < g.Hn;
     const int k = valid ? logical : g.Hn - 1;   // list row (canvas row rb + k)
-    const int Wc = g.W + 4, xs = g.x0 - 2;
+    // state / synthesis window: canvas columns x0 - 2 .. x0 + Wy + 1 (the blur's
+    // reach around the Yh columns; Wy = W + 1 for odd W: the crop's second texel)
+    const int Wc = g.Wy + 4, xs = g.x0 - 2;
     const int nmid = sp.L >= 3 ? sp.L - 2 : 0;
     const int nb = nmid * (sp.O / 2);
     constexpr bool iir = IIR;
@@ -421,7 +423,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     }
     // |y| (ConvertComplexMagToTex) then the horizontal half of ApplyAntiAliasing
     float *raw = reinterpret_cast<float *>(lds);
-    const bool interior = g.x0 >= 2 && g.x0 + g.W + 2 <= N;
+    const bool interior = g.x0 >= 2 && g.x0 + g.Wy + 2 <= N;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
         if (!((write_mask >> f) & 1)) continue;   // uniform
@@ -430,8 +432,8 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
         for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[f][j]);
         __syncthreads();
         if (valid) {
-            float *out = Yh + (size_t)f * yh_stride + (size_t)k * g.W;
-            for (int X = t0; X < g.W; X += T) {
+            float *out = Yh + (size_t)f * yh_stride + (size_t)k * g.Wy;
+            for (int X = t0; X < g.Wy; X += T) {
                 const int c = g.x0 + X;
                 float acc;
                 if (interior) {

@@ -39,13 +39,17 @@ def test_create_rejects_bad_arguments_without_gpu():
     h = ctypes.c_void_p()
     L = mm355.lib()
     st = mm355.Params.make(mode=mm355.MODE_STEERABLE, orientations=8)
-    assert L.mm_create(63, 48, ctypes.byref(st), 0, ctypes.byref(h)) == -2  # odd width: steerable only
     assert L.mm_create(8193, 48, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N > 8192
     assert L.mm_create(5120, 48, ctypes.byref(st), 0, ctypes.byref(h)) == -2  # steerable: N <= 4096
     assert L.mm_create(16385, 2160, ctypes.byref(p), 0, ctypes.byref(h)) == -2  # N = 32768
     assert L.mm_create(8, 6, ctypes.byref(p), 0, ctypes.byref(h)) == -2      # N = 8 < 16
     assert L.mm_create(2, 2, ctypes.byref(p), 0, ctypes.byref(h)) == -2      # N = 2
     assert not h.value                                                       # nothing created
+    # odd sizes are accepted in steerable mode too (round 5): only the device is missing here
+    assert L.mm_create(63, 47, ctypes.byref(st), 0, ctypes.byref(h)) in (-4, 0)
+    if h.value:
+        L.mm_destroy(h)
+        h = ctypes.c_void_p()
     bad = mm355.Params.make()
     bad.orientations = 8
     assert L.mm_create(64, 48, ctypes.byref(bad), 0, ctypes.byref(h)) == -2

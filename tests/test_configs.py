@@ -52,6 +52,21 @@ def test_c2_steerable_o8_1080p_vs_spec(filt):
 
 
 @pytest.mark.slow
+def test_steerable_o8_1919x1079_vs_spec():
+    """An odd full-size screen in the steerable extension (round 5: odd W and
+    H accepted): 1919x1079 (N = 2048, the quad half a texel off the grid in
+    both directions), L=5, O=8 DIFF, S=25, 3 frames in batches of 2."""
+    W, H, n = 1919, 1079, 3
+    fr = _f32(W, H, n)
+    got = gpu_steer(W, H, fr, levels=5, S=25.0, Oo=8, filt=SR.FILTER_DIFF, batch=2)
+    r = SR.SteerableRef(W, H, levels=5, phase_scale=25.0, orientations=8, filt=SR.FILTER_DIFF)
+    ref = [r.process(f.astype(np.float64)) for f in fr]
+    assert np.array_equal(got[0], fr[0])
+    for k in range(1, n):
+        _close_spec(got[k], ref[k])
+
+
+@pytest.mark.slow
 def test_c3_2160p_rgba8_stream_across_batches():
     """C3 geometry (N = 4096), reference semantics: an RGBA8 stream of 6 frames
     in batches of 4 (K2's state stored and reloaded at the boundary) against

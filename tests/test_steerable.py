@@ -79,9 +79,8 @@ def gpu_steer(W, H, fr, levels=5, S=10.0, Oo=8, filt=0, rl=0.05, rh=0.4, edge=0,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Oo,filt", [(8, 0), (4, 1)])
-def test_gpu_s0_equals_reference_oracle(Oo, filt):
-    W, H = 96, 64
+@pytest.mark.parametrize("Oo,filt,W,H", [(8, 0, 96, 64), (4, 1, 96, 64), (8, 0, 95, 63), (6, 1, 96, 63)])
+def test_gpu_s0_equals_reference_oracle(Oo, filt, W, H):
     fr = frames(W, H, 4)
     got = gpu_steer(W, H, fr, S=0.0, Oo=Oo, filt=filt)
     ref = T.oracle_run(W, H, fr, levels=5, S=0.0)
@@ -100,7 +99,11 @@ def _close_spec(got, ref):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,H,Oo,filt,S,edge", [(64, 48, 8, 0, 10.0, 0), (96, 64, 4, 1, 25.0, 0),
-                                                 (64, 48, 6, 1, 9.7, 1), (200, 120, 8, 0, 25.0, 0)])
+                                                 (64, 48, 6, 1, 9.7, 1), (200, 120, 8, 0, 25.0, 0),
+                                                 # odd sizes: the quad half a texel off the grid
+                                                 (63, 47, 8, 0, 10.0, 0), (97, 63, 4, 1, 25.0, 1),
+                                                 (65, 48, 6, 0, 9.7, 0), (64, 49, 8, 1, 10.0, 1),
+                                                 (199, 121, 8, 0, 25.0, 0)])
 def test_gpu_matches_spec(W, H, Oo, filt, S, edge):
     n = 5
     fr = frames(W, H, n)
@@ -113,13 +116,14 @@ def test_gpu_matches_spec(W, H, Oo, filt, S, edge):
 
 
 @pytest.mark.gpu
-def test_gpu_chunked_and_state_handoff():
+@pytest.mark.parametrize("W,H", [(64, 48), (63, 47)])
+def test_gpu_chunked_and_state_handoff(W, H):
     """Batch boundaries (mm_set_batch 4) and the DIFF state hand-off:
     a second handle seeded with mm_compute_state(frame k-1) continues the
     stream bitwise; mm_get_state/mm_set_state carry the IIR state."""
     import mm355
     import torch
-    W, H, n = 64, 48, 11
+    n = 11
     fr = frames(W, H, n)
     dev = torch.from_numpy(np.stack(fr)).cuda()
     for filt in (0, 1):
