@@ -103,7 +103,9 @@ def _close_spec(got, ref):
                                                  # odd sizes: the quad half a texel off the grid
                                                  (63, 47, 8, 0, 10.0, 0), (97, 63, 4, 1, 25.0, 1),
                                                  (65, 48, 6, 0, 9.7, 0), (64, 49, 8, 1, 10.0, 1),
-                                                 (199, 121, 8, 0, 25.0, 0)])
+                                                 (199, 121, 8, 0, 25.0, 0),
+                                                 # tiny canvases (N = 32, 16): one wave per transform
+                                                 (31, 16, 8, 1, 10.0, 0), (15, 9, 4, 0, 10.0, 1)])
 def test_gpu_matches_spec(W, H, Oo, filt, S, edge):
     n = 5
     fr = frames(W, H, n)
