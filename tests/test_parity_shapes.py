@@ -154,3 +154,40 @@ def test_n8192_f32_vs_oracle(W, H, L, S):
         assert np.array_equal(got[0], fr[0])
         for k in range(1, 3):
             T.assert_close_f32(got[k], ref[k], integer_scale=float(S).is_integer())
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_c3_launch_shape_vs_oracle():
+    """C3's K2 launch shapes (3840x2160, L = 6: the two-band op at N = 4096,
+    the 30 % packed-block tail share and the second-half tails), 60 RGBA8
+    frames in one mm_process_stream call at batch 30: every frame where a
+    batch's launch shape changes (the prime from the state slot, the hand-offs
+    to k_cols_tail and to the second-half tails, the last frame) against the
+    oracle fed frames t-1 and t, frame 0 bitwise."""
+    import torch
+    import mm355
+    W, H, C, B, L, S = 3840, 2160, 60, 30, 6, 25.0
+    O.set_threads(16)
+    h = mm355.Handle(W, H, mm355.Params.make(levels=L, phase_scale=S))
+    h.set_batch(B)
+    fr = torch.empty((C, H, W, 4), dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(fr)
+    h.synth(fr, 0, C, seed=0x5EED0000)
+    h.process_stream(fr, out, C, mm355.RGBA8)
+    torch.cuda.synchronize()
+    h.close()
+    assert np.array_equal(out[0].cpu().numpy(), fr[0].cpu().numpy())
+    ts = set()
+    for b in range(0, C, B):
+        nf = min(B, C - b)
+        k = max(0, min(nf * 30 // 100, nf - 2))     # packed-block frames in k_cols_tail (N = 4096)
+        k2t = min(nf * 10 // 100, nf - 2)           # second-half tails
+        ts |= {b, b + 1, b + nf - k - 1, b + nf - k, b + nf - k2t - 1, b + nf - k2t, b + nf - 1}
+    ts.discard(0)
+    assert len(ts) >= 12
+    for t in sorted(ts):
+        pair = [O.synth_frame(W, H, t - 1), O.synth_frame(W, H, t)]
+        assert np.array_equal(pair[1], fr[t].cpu().numpy())
+        ref = _oracle_at(W, H, pair, 1, levels=L, phase_scale=S)
+        T.assert_close_u8(out[t].cpu().numpy(), ref)
