@@ -634,10 +634,14 @@ def main():
                 allv = [mine]
             if rank == 0:
                 print(json.dumps({"checksums_by_rank": {str(r): v for r, v in enumerate(allv)},
-                                  "world": world}), flush=True)
+                                  "world": world, "inputs_wrapped": nbuf < total_steps}), flush=True)
         elif rank == 0:
+            # inputs_wrapped: the resident buffers repeat (step s reads s mod nbuf),
+            # so the sums are not those of the single-rank stream of that length
+            # and a ring-vs-single comparison must not trust them
             print(json.dumps({"checksums": [sums[k] for k in sorted(sums)],
-                              "frames": sorted(sums)[:1] + sorted(sums)[-1:], "world": world}),
+                              "frames": sorted(sums)[:1] + sorted(sums)[-1:], "world": world,
+                              "inputs_wrapped": nbuf < total_steps}),
                   flush=True)
         if world > 1:
             dist.destroy_process_group()
@@ -704,6 +708,9 @@ def main():
                                 f"{W}x{H} RGBA8 synthetic stream, {a.levels}-level pyramid, "
                                 f"PhaseScale={a.phase_scale}, orientations=1 (reference semantics)"),
                    "frames_per_step_per_gpu": C, "padded_n": N,
+                   # step s reads resident buffer s mod nbuf: past nbuf steps the
+                   # synthetic stream repeats (every step still moves its bytes)
+                   "inputs_wrapped": nbuf < total_steps,
                    "call_pattern": ("one mm_process per frame (batch 1)" if per_frame else
                                     f"mm_process_stream, {C} frames per call in batches of {B}"),
                    "parallelism": ("single GPU" if world == 1 and not c_ring else

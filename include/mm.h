@@ -12,9 +12,11 @@
  *   - Every function returns MM_OK (0) or a negative MM_ERR_* code; nothing
  *     throws or aborts across the ABI.  mm_strerror() names a code.
  *   - Frames are caller-owned, row-major, H rows of W RGBA pixels, tightly
- *     packed (pitch = W * bytes-per-pixel).  RGBA8 is UNORM (v = byte/255);
- *     RGBA32F is linear float.  The handle owns all device scratch and the
- *     one-frame temporal state.
+ *     packed (pitch = W * bytes-per-pixel, mm_frame_bytes).  RGBA8 is UNORM
+ *     (v = byte/255); RGBA32F and RGBA16F are linear float; RGBA8_SRGB is an
+ *     8-bit sRGB target as Unity's Linear colour space sees it (decoded to
+ *     linear light on read, encoded on write).  The handle owns all device
+ *     scratch and the one-frame temporal state.
  *   - A handle is not thread-safe: one handle per video stream, calls in frame
  *     order (Unity calls OnRenderImage serially on its render thread).
  *   - The first frame after mm_create/mm_reset is passed through bitwise
@@ -39,9 +41,10 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 9   /* 8: the state is G_{t-1} (row spectra), see mm_state_size;
+#define MM_ABI_VERSION 10  /* 8: the state is G_{t-1} (row spectra), see mm_state_size;
                               9: handle-scoped teardown and batch changes (mm_destroy,
-                                 mm_set_batch), no device-wide synchronisation */
+                                 mm_set_batch), no device-wide synchronisation;
+                             10: MM_RGBA16F and MM_RGBA8_SRGB frames, mm_frame_bytes */
 
 /* error codes */
 #define MM_OK               0
@@ -52,9 +55,23 @@ extern "C" {
 #define MM_ERR_OOM         -5  /* device allocation failed */
 #define MM_ERR_NO_STATE    -6  /* mm_get_state before any frame was seen */
 
-/* frame formats */
-#define MM_RGBA8   0
-#define MM_RGBA32F 1
+/* frame formats (every entry point that takes frames takes each of them) */
+#define MM_RGBA8   0       /* 4 B/px, UNORM: v = byte / 255; out round(saturate(v) * 255) */
+#define MM_RGBA32F 1       /* 16 B/px, linear float                                       */
+/* The frames the reference actually receives (since ABI 10): its camera
+ * renders HDR (Assets/Scenes/SampleScene.unity:663, m_HDR: 1) in Linear colour
+ * space (ProjectSettings/ProjectSettings.asset:50, m_ActiveColorSpace: 1), so
+ * OnRenderImage's source (.cs:101) is a linear half-float target (values may
+ * exceed 1) that .cs:109 blits into ARGBFloat; an LDR camera's 8-bit target is
+ * sRGB, sampled as linear light and encoded on write. */
+#define MM_RGBA16F    2    /* 8 B/px, linear IEEE half; values above 1 pass until the
+                              reference's saturate (YIQToRGB); out rounded to nearest
+                              even half, alpha 1.0                                   */
+#define MM_RGBA8_SRGB 3    /* 4 B/px, sRGB-encoded bytes: in = the exact IEC 61966-2-1
+                              decode of each byte (a 256-entry fp32 table), the whole
+                              pipeline in linear light, out = the byte whose sRGB
+                              interval holds saturate(v) (halfway points in linear
+                              light; tools/gen_srgb.py); alpha byte / 255, out 255    */
 
 /* mm_params.mode */
 #define MM_MODE_PYRAMID   0   /* usePyramidDecomposition = true (.cs:18, :128-131) */
@@ -133,6 +150,10 @@ int mm_get_params(const mm_handle *h, mm_params *p);
 
 /* Padded FFT size N (.cs:300-302). */
 int mm_padded_size(const mm_handle *h, int *n);
+
+/* Bytes of one W x H frame of `format` (MM_ERR_INVALID for an unknown format
+ * or size).  Since ABI 10. */
+int mm_frame_bytes(int width, int height, int format, size_t *bytes);
 
 /* OnRenderImage (.cs:101-143): one frame in, one frame out.
  * flags & MM_FRAMES_ON_DEVICE: in/out are device pointers and the call is

@@ -73,10 +73,22 @@ int mm_ring_step(mm_ring *r, int step, const void *in, void *out, const void *ne
  * falls as (1 - iir_low)^halo_frames: mm_ring_halo_frames() picks the halo at
  * which that factor is 1e-6 (270 frames at iir_low = 0.05), where RGBA8
  * outputs meet the parity bar (<= 1 LSB on <= 0.1 % of values; tests/test_ring_c.py).
- * Nothing crosses the ring in this mode.  mm_ring_step refuses IIR handles. */
+ * Nothing crosses the ring in this mode.  mm_ring_step refuses IIR handles.
+ * Cost: every rank re-runs halo_frames frames per chunk, i.e. halo_frames /
+ * chunk extra work (90 % at the default 270-frame halo and 300-frame chunks);
+ * the halo buffer the caller keeps is halo_frames frames.
+ * mm_ring_halo_frames: ceil(ln 1e-6 / ln(1 - iir_low)) in closed form, 0 for
+ * a non-IIR ring; MM_ERR_UNSUPPORTED above MM_RING_HALO_MAX frames (iir_low
+ * below about 0.0067: the halo would dwarf any chunk). */
+#define MM_RING_HALO_MAX 2048
 int mm_ring_step_halo(mm_ring *r, int step, const void *halo, int halo_frames, const void *in, void *out,
                       void *hip_stream);
 int mm_ring_halo_frames(const mm_ring *r, int *frames);
+
+/* Path of the libmm355 this library's mm_* calls are bound to (dladdr), for
+ * callers that load a specific build of the operator (mm355/ring.py refuses
+ * a ring bound to another build than the one it loaded).  NULL if unknown. */
+const char *mm_ring_core_library(void);
 
 /* Waits for every posted shift (a shift posted for a step that is never run
  * included) and releases the ring. */

@@ -754,6 +754,114 @@ void mm_ref_process_u8(mm_ref *c, const uint8_t *in, uint8_t *out)
 }
 
 /* ------------------------------------------------------------------ */
+/* the engine's other frame formats (include/mm.h MM_RGBA16F, MM_RGBA8_SRGB) */
+/* ------------------------------------------------------------------ */
+/* The reference camera renders HDR (SampleScene.unity:663, m_HDR: 1) in Linear
+ * colour space (ProjectSettings.asset:50): OnRenderImage's source (.cs:101) is
+ * a linear half-float target that .cs:109 blits into ARGBFloat, i.e. the
+ * float pipeline above sees the half values exactly; the destination write
+ * rounds to half.  An 8-bit target in Linear colour space is sRGB: sampled as
+ * linear light (IEC 61966-2-1 decode), encoded on write. */
+float mm_ref_half_to_float(uint16_t h)
+{
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    uint32_t b;
+    if (e == 0) {                                          /* zero / subnormal: m 2^-24 */
+        float v = ldexpf((float)m, -24);
+        return s ? -v : v;
+    }
+    if (e == 31) b = s | 0x7f800000u | (m << 13);          /* inf / NaN */
+    else b = s | ((e - 15 + 127) << 23) | (m << 13);
+    float f;
+    memcpy(&f, &b, 4);
+    return f;
+}
+
+/* IEEE binary16, round to nearest even (what the destination write does) */
+uint16_t mm_ref_float_to_half(float f)
+{
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | (ax > 0x7f800000u ? 0x7e00u : 0x7c00u));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);   /* >= 65520: inf */
+    if (ax < 0x38800000u) {                                      /* below 2^-14: subnormal */
+        float a;
+        memcpy(&a, &ax, 4);
+        return (uint16_t)(sign | (uint32_t)rintf(a * 16777216.0f));   /* exact scale, RNE */
+    }
+    uint32_t h = ((((ax >> 23) - 127 + 15) << 10) | ((ax & 0x7fffffu) >> 13));
+    const uint32_t rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+}
+
+static double srgb_lin(double c)
+{
+    return c <= 0.04045 ? c / 12.92 : pow((c + 0.055) / 1.055, 2.4);
+}
+
+/* dec[b] = lin(b/255); thr[b] = lin((b - 0.5)/255) (b = 1..255), thr[0] = -inf,
+ * thr[256] = +inf: double formula rounded to fp32 (tools/gen_srgb.py states
+ * the same tables for the kernels) */
+void mm_ref_srgb_tables(float *dec, float *thr)
+{
+    for (int b = 0; b < 256; ++b) dec[b] = (float)srgb_lin(b / 255.0);
+    thr[0] = -HUGE_VALF;
+    for (int b = 1; b < 256; ++b) thr[b] = (float)srgb_lin((b - 0.5) / 255.0);
+    thr[256] = HUGE_VALF;
+}
+
+/* the byte whose sRGB interval holds v (largest b with v >= thr[b]) */
+static uint8_t srgb_encode(const float *thr, float v)
+{
+    int lo = 0, hi = 255;                                   /* thr[lo] <= v always */
+    while (lo < hi) {
+        int mid = (lo + hi + 1) / 2;
+        if (v >= thr[mid]) lo = mid;
+        else hi = mid - 1;
+    }
+    return (uint8_t)lo;
+}
+
+void mm_ref_process_f16(mm_ref *c, const uint16_t *in, uint16_t *out)
+{
+    const size_t px = (size_t)c->W * c->H * 4;
+    float *fi = (float *)malloc(sizeof(float) * px);
+    float *fo = (float *)malloc(sizeof(float) * px);
+    if (!fi || !fo) { free(fi); free(fo); return; }
+    int passthrough = c->first || (!c->apply && !c->show_mag && !c->show_phase);
+    for (size_t i = 0; i < px; ++i) fi[i] = mm_ref_half_to_float(in[i]);
+    mm_ref_process(c, fi, fo, NULL);
+    if (passthrough) memcpy(out, in, sizeof(uint16_t) * px);   /* bitwise copy */
+    else
+        for (size_t i = 0; i < px; ++i) out[i] = mm_ref_float_to_half(fo[i]);
+    free(fi);
+    free(fo);
+}
+
+void mm_ref_process_srgb8(mm_ref *c, const uint8_t *in, uint8_t *out)
+{
+    const size_t px = (size_t)c->W * c->H * 4;
+    float dec[256], thr[257];
+    mm_ref_srgb_tables(dec, thr);
+    float *fi = (float *)malloc(sizeof(float) * px);
+    float *fo = (float *)malloc(sizeof(float) * px);
+    if (!fi || !fo) { free(fi); free(fo); return; }
+    int passthrough = c->first || (!c->apply && !c->show_mag && !c->show_phase);
+    for (size_t i = 0; i < px; ++i)                        /* alpha is linear in sRGB targets */
+        fi[i] = (i & 3) == 3 ? (float)in[i] / 255.0f : dec[in[i]];
+    mm_ref_process(c, fi, fo, NULL);
+    if (passthrough) memcpy(out, in, px);                  /* bitwise copy */
+    else
+        for (size_t i = 0; i < px; ++i)
+            out[i] = (i & 3) == 3 ? (uint8_t)(saturatef(fo[i]) * 255.0f + 0.5f)
+                                  : srgb_encode(thr, saturatef(fo[i]));
+    free(fi);
+    free(fo);
+}
+
+/* ------------------------------------------------------------------ */
 /* synthetic stream                                      */
 /* ------------------------------------------------------------------ */
 static uint64_t splitmix64(uint64_t x)

@@ -73,6 +73,16 @@ void    mm_ref_process(mm_ref *ctx, const float *in_rgba, float *out_rgba,
 /* Same on RGBA8 frames: in = u8/255 (UNORM), out = round(saturate(v)*255). */
 void    mm_ref_process_u8(mm_ref *ctx, const uint8_t *in_rgba, uint8_t *out_rgba);
 
+/* Linear half frames (MM_RGBA16F, IEEE binary16 bits): in decoded exactly,
+ * out rounded to nearest even; first frame bitwise.                         */
+void    mm_ref_process_f16(mm_ref *ctx, const uint16_t *in_rgba, uint16_t *out_rgba);
+/* 8-bit sRGB frames (MM_RGBA8_SRGB): in = dec[byte] (alpha byte/255), out =
+ * the byte whose sRGB interval holds saturate(v) (alpha 255).              */
+void    mm_ref_process_srgb8(mm_ref *ctx, const uint8_t *in_rgba, uint8_t *out_rgba);
+void    mm_ref_srgb_tables(float *dec256, float *thr257);
+float   mm_ref_half_to_float(uint16_t h);
+uint16_t mm_ref_float_to_half(float f);
+
 /* showMagnitude / showPhase (.cs:13-14): ProcessDebugView (.cs:234-257)
  * replaces the magnified output while either is set (state still follows
  * the input, .cs:122).                                                      */

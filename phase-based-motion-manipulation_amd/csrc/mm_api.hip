@@ -355,7 +355,9 @@ int mm_set_params(mm_handle *h, const mm_params *p)
     if (!h) return MM_ERR_INVALID;
     int rc = validate_params(p);
     if (rc) return rc;
-    if (p->mode == MM_MODE_STEERABLE && (h->geo.ox || h->geo.oy || h->N > 4096)) return MM_ERR_UNSUPPORTED;
+    // the band kernels run two transforms per workgroup (N <= 4096); odd sizes
+    // are supported in every mode since round 5 (as mm_create accepts them)
+    if (p->mode == MM_MODE_STEERABLE && h->N > 4096) return MM_ERR_UNSUPPORTED;
     const bool edge_changed = p->edge_mode != h->p.edge_mode;
     DEVICE_SCOPE(h);
     // Kernels take the parameters by value at launch, so only a table rewrite
@@ -393,6 +395,13 @@ int mm_padded_size(const mm_handle *h, int *n)
     return MM_OK;
 }
 
+int mm_frame_bytes(int width, int height, int format, size_t *bytes)
+{
+    if (!bytes || width < 1 || height < 1 || !fmt_valid(format)) return MM_ERR_INVALID;
+    *bytes = (size_t)width * (size_t)height * fmt_bpp(format);
+    return MM_OK;
+}
+
 void *mm_stream(mm_handle *h) { return h ? (void *)h->stream : nullptr; }
 
 int mm_set_batch(mm_handle *h, int frames)
@@ -416,7 +425,7 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
                       void *hip_stream)
 {
     if (!h || !in || !out || count < 0) return MM_ERR_INVALID;
-    if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
+    if (!fmt_valid(format)) return MM_ERR_INVALID;
     if (count == 0) return MM_OK;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
@@ -432,10 +441,10 @@ int mm_process_stream(mm_handle *h, const void *in, void *out, int count, int fo
 int mm_process(mm_handle *h, const void *in, void *out, int format, int flags, void *hip_stream)
 {
     if (!h || !in || !out) return MM_ERR_INVALID;
-    if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
+    if (!fmt_valid(format)) return MM_ERR_INVALID;
     if (flags & MM_FRAMES_ON_DEVICE) return mm_process_stream(h, in, out, 1, format, hip_stream);
     // host frames: stage through device buffers and synchronise
-    const size_t fb = (size_t)h->W * h->H * (format ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(format);
     DEVICE_SCOPE(h);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     int ro = order_after_last(h, s);
@@ -525,7 +534,7 @@ int mm_compute_state(mm_handle *h, const void *in_dev, int format, void *dev_buf
 {
     size_t need = 0;
     if (!h || !in_dev || !dev_buf || mm_state_size(h, &need) || bytes < need) return MM_ERR_INVALID;
-    if (format != MM_RGBA8 && format != MM_RGBA32F) return MM_ERR_INVALID;
+    if (!fmt_valid(format)) return MM_ERR_INVALID;
     hipStream_t s = (hipStream_t)hip_stream;   // NULL: the default stream (HIP convention)
     DEVICE_SCOPE(h);
     // the IIR state is a history of frames, not a function of one input frame

@@ -203,6 +203,25 @@ struct ProfScope {
     }
 };
 
+// Bytes per pixel of a frame format (include/mm.h); the kernels' FMT template
+// argument is the format code itself (Pix<FMT>, mm_kernels.hpp).
+static inline size_t fmt_bpp(int fmt)
+{
+    return fmt == MM_RGBA32F ? 16 : fmt == MM_RGBA16F ? 8 : 4;
+}
+static inline bool fmt_valid(int fmt)
+{
+    return fmt == MM_RGBA8 || fmt == MM_RGBA32F || fmt == MM_RGBA16F || fmt == MM_RGBA8_SRGB;
+}
+// Runs the statement with the compile-time format FMT_ of the runtime `fmt`.
+#define MM_FMT_SWITCH(fmt, ...)                                                \
+    switch (fmt) {                                                             \
+    case MM_RGBA8: { constexpr int FMT_ = MM_RGBA8; __VA_ARGS__; } break;      \
+    case MM_RGBA32F: { constexpr int FMT_ = MM_RGBA32F; __VA_ARGS__; } break;  \
+    case MM_RGBA16F: { constexpr int FMT_ = MM_RGBA16F; __VA_ARGS__; } break;  \
+    default: { constexpr int FMT_ = MM_RGBA8_SRGB; __VA_ARGS__; } break;       \
+    }
+
 // ------------------------------------------------------------------------
 // host tables
 // ------------------------------------------------------------------------
@@ -414,10 +433,9 @@ static int set_attrs(int W)
     (void)W;   // every other kernel stays within the default 64 KiB dynamic LDS
     if constexpr (LOG2N == 12) {   // k_rows_inv_compose: two 4096-point groups, 73.7 KB
         const int lds = (int)(sizeof(c2) * 2 * lds_complex<4096>());
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, 0>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, 1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        for (int f = 0; f < 4; ++f)
+            MM_FMT_SWITCH(f, HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, FMT_>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds)))
     }
     if constexpr (LOG2N == 13) {   // N = 8192: one 8192-point transform per workgroup, 73.7 KB and more
         auto set = [](const void *f, size_t b) {
@@ -442,10 +460,9 @@ static int set_attrs(int W)
     }
     if constexpr (LOG2N == 11) {   // k_rows_inv_compose4: four 2048-point groups, 73.7 KB
         const int lds = (int)(sizeof(c2) * 4 * lds_complex<2048>());
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose4<11, 0>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose4<11, 1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        for (int f = 0; f < 4; ++f)
+            MM_FMT_SWITCH(f, HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose4<11, FMT_>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds)))
     }
     return MM_OK;
 }
@@ -457,7 +474,7 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
     const int total = ppf * nframes;
     // fewer than 2 workgroups per CU at the batch form: the one-pair form
     const bool lat = (total + k1_groups<LOG2N>() - 1) / k1_groups<LOG2N>() < 512;
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     ProfScope ps(h, s, MM_K_ROWS_FWD, nframes);
 #define MM_K1_LAUNCH(F, GEN, LAT)                                                                  \
     do {                                                                                           \
@@ -471,15 +488,9 @@ static int launch_k1(mm_handle *h, const uint8_t *in, int nframes, int fmt, hipS
                            h->d_col3, h->d_row3, h->d_col, h->d_row, h->d_tw, G, h->g_stride);     \
     } while (0)
     const bool gen = h->geo.ox || h->geo.oy;   // odd W/H: taps span i-2 .. i+1
-    if (fmt == MM_RGBA8) {
-        if (gen) MM_K1_LAUNCH(0, true, false);
-        else if (lat) MM_K1_LAUNCH(0, false, true);
-        else MM_K1_LAUNCH(0, false, false);
-    } else {
-        if (gen) MM_K1_LAUNCH(1, true, false);
-        else if (lat) MM_K1_LAUNCH(1, false, true);
-        else MM_K1_LAUNCH(1, false, false);
-    }
+    MM_FMT_SWITCH(fmt, if (gen) MM_K1_LAUNCH(FMT_, true, false);
+                       else if (lat) MM_K1_LAUNCH(FMT_, false, true);
+                       else MM_K1_LAUNCH(FMT_, false, false))
 #undef MM_K1_LAUNCH
     HIPCHK(hipGetLastError());
     return MM_OK;
@@ -635,7 +646,7 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
 {
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     const int R = k34_strip_rows(h, nout);
     // Short launches (the one-frame call) at N <= 1024 whose strips fit one
     // workgroup round (4 waves per SIMD at <= 128 VGPRs: 1024 / 4T workgroups
@@ -654,12 +665,9 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
         const size_t lds = sizeof(c2) * 4 * lds_complex<(1 << LOG2N)>();
         const dim3 grid((unsigned)(strips * nout)), block(4 * fft_T<LOG2N>());
         ProfScope ps(h, s, MM_K_ROWS_INV_COMPOSE, nout);
-        if (fmt == MM_RGBA8)
-            hipLaunchKernelGGL((k_rows_inv_compose4<LOG2N, 0>), grid, block, lds, s, h->d_Q, h->q_stride,
-                               in, out, fb, frame0, strips, h->geo, h->blur, h->d_col3, h->d_row3, h->d_tw);
-        else
-            hipLaunchKernelGGL((k_rows_inv_compose4<LOG2N, 1>), grid, block, lds, s, h->d_Q, h->q_stride,
-                               in, out, fb, frame0, strips, h->geo, h->blur, h->d_col3, h->d_row3, h->d_tw);
+        MM_FMT_SWITCH(fmt, hipLaunchKernelGGL((k_rows_inv_compose4<LOG2N, FMT_>), grid, block, lds, s, h->d_Q,
+                                              h->q_stride, in, out, fb, frame0, strips, h->geo, h->blur,
+                                              h->d_col3, h->d_row3, h->d_tw))
         HIPCHK(hipGetLastError());
         return MM_OK;
     }
@@ -668,14 +676,9 @@ static int launch_k3(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
         const size_t lds = sizeof(c2) * 2 * lds_complex<(1 << LOG2N)>();
         const dim3 grid((unsigned)(strips * nout)), block(2 * fft_T<LOG2N>());
         ProfScope ps(h, s, MM_K_ROWS_INV_COMPOSE, nout);
-        if (fmt == MM_RGBA8)
-            hipLaunchKernelGGL((k_rows_inv_compose<LOG2N, 0>), grid, block, lds, s, h->d_Q, h->q_stride,
-                               in, out, fb, frame0, strips, steps, h->geo, h->blur, h->d_col3,
-                               h->d_row3, h->d_tw);
-        else
-            hipLaunchKernelGGL((k_rows_inv_compose<LOG2N, 1>), grid, block, lds, s, h->d_Q, h->q_stride,
-                               in, out, fb, frame0, strips, steps, h->geo, h->blur, h->d_col3,
-                               h->d_row3, h->d_tw);
+        MM_FMT_SWITCH(fmt, hipLaunchKernelGGL((k_rows_inv_compose<LOG2N, FMT_>), grid, block, lds, s, h->d_Q,
+                                              h->q_stride, in, out, fb, frame0, strips, steps, h->geo,
+                                              h->blur, h->d_col3, h->d_row3, h->d_tw))
         HIPCHK(hipGetLastError());
         return MM_OK;
     }
@@ -702,29 +705,23 @@ static int launch_k4(mm_handle *h, const uint8_t *in, uint8_t *out, int frame0, 
 {
     const int nout = nframes - frame0;
     if (nout <= 0) return MM_OK;
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     if (h->geo.ox || h->geo.oy) {   // odd W/H: the crop samples between texels
         const size_t tot = (size_t)nout * h->W * h->H;
         ProfScope ps(h, s, MM_K_COMPOSE, nout);
         const dim3 grid((unsigned)((tot + 255) / 256));
-        if (fmt == MM_RGBA8)
-            hipLaunchKernelGGL((k_compose_odd<0>), grid, dim3(256), 0, s, h->d_Yh, h->yh_stride, in, out,
-                               fb, frame0, nout, h->geo, h->blur, h->d_col, h->d_row);
-        else
-            hipLaunchKernelGGL((k_compose_odd<1>), grid, dim3(256), 0, s, h->d_Yh, h->yh_stride, in, out,
-                               fb, frame0, nout, h->geo, h->blur, h->d_col, h->d_row);
+        MM_FMT_SWITCH(fmt, hipLaunchKernelGGL((k_compose_odd<FMT_>), grid, dim3(256), 0, s, h->d_Yh,
+                                              h->yh_stride, in, out, fb, frame0, nout, h->geo, h->blur,
+                                              h->d_col, h->d_row))
         HIPCHK(hipGetLastError());
         return MM_OK;
     }
     const int rt = (h->H + kTileRows - 1) / kTileRows, ct = (h->W + kTileCols - 1) / kTileCols;
     const dim3 grid(rt * ct * nout);
     ProfScope ps(h, s, MM_K_COMPOSE, nout);
-    if (fmt == MM_RGBA8)
-        hipLaunchKernelGGL((k_compose<0>), grid, dim3(kTileCols), 0, s, h->d_Yh, h->yh_stride,
-                           in, out, fb, frame0, rt, ct, h->geo, h->blur, h->d_col3, h->d_row3);
-    else
-        hipLaunchKernelGGL((k_compose<1>), grid, dim3(kTileCols), 0, s, h->d_Yh, h->yh_stride,
-                           in, out, fb, frame0, rt, ct, h->geo, h->blur, h->d_col3, h->d_row3);
+    MM_FMT_SWITCH(fmt, hipLaunchKernelGGL((k_compose<FMT_>), grid, dim3(kTileCols), 0, s, h->d_Yh,
+                                          h->yh_stride, in, out, fb, frame0, rt, ct, h->geo, h->blur,
+                                          h->d_col3, h->d_row3))
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -843,7 +840,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         k += nf;
     }
     if (sst == h->d_sst) h->steer_valid = true;
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     if (!write) {
         if (out) HIPCHK(hipMemcpyAsync(out, in, fb * n, hipMemcpyDeviceToDevice, s));
         return MM_OK;
@@ -883,15 +880,11 @@ static int run_debug(mm_handle *h, uint8_t *out, int n, int first, int fmt, hipS
                        tex_stride, first, h->p.show_magnitude, h->p.show_phase, h->geo,
                        h->d_tw_half);
     HIPCHK(hipGetLastError());
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     const size_t tot = (size_t)m * h->W * h->H;
     const dim3 grid((unsigned)((tot + 255) / 256));
-    if (fmt == MM_RGBA8)
-        hipLaunchKernelGGL((k_dbg_out<0>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
-                           first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
-    else
-        hipLaunchKernelGGL((k_dbg_out<1>), grid, dim3(256), 0, s, h->d_dbg, tex_stride, out, fb,
-                           first, m, h->p.show_magnitude, h->p.show_phase, h->geo);
+    MM_FMT_SWITCH(fmt, hipLaunchKernelGGL((k_dbg_out<FMT_>), grid, dim3(256), 0, s, h->d_dbg, tex_stride,
+                                          out, fb, first, m, h->p.show_magnitude, h->p.show_phase, h->geo))
     HIPCHK(hipGetLastError());
     return MM_OK;
 }
@@ -901,7 +894,7 @@ template <int LOG2N>
 static int run_chunk(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int fmt,
                      hipStream_t s)
 {
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     const bool mag = h->p.apply_magnification != 0;
     const bool dbg = h->p.show_magnitude || h->p.show_phase;
     // the steerable path's state is its local-phase planes; every other path
@@ -953,7 +946,7 @@ template <int LOG2N>
 static int run_stream(mm_handle *h, const uint8_t *in, uint8_t *out, int count, int fmt,
                       hipStream_t s)
 {
-    const size_t fb = (size_t)h->W * h->H * (fmt ? 16 : 4);
+    const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);
     for (int f0 = 0; f0 < count; f0 += h->chunk) {
         const int n = std::min(h->chunk, count - f0);
         int rc = run_chunk<LOG2N>(h, in + fb * f0, out + fb * f0, n, fmt, s);

@@ -16,6 +16,7 @@
 // bin serves every level.
 #pragma once
 #include "mm_fft.hpp"
+#include "mm_srgb.hpp"
 #include <stdint.h>
 #include <type_traits>
 
@@ -164,12 +165,17 @@ __device__ __forceinline__ void st_stream(void *base, unsigned byte_off, T v)
 {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     void *p = reinterpret_cast<uint8_t *>(base) + byte_off;
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     if constexpr (sizeof(T) == 16) {
         u32x4 w;
         __builtin_memcpy(&w, &v, 16);
         __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+    } else if constexpr (sizeof(T) == 8) {
+        u32x2 w;
+        __builtin_memcpy(&w, &v, 8);
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x2 *>(p));
     } else {
-        static_assert(sizeof(T) == 4, "st_stream: 4 or 16 bytes");
+        static_assert(sizeof(T) == 4, "st_stream: 4, 8 or 16 bytes");
         unsigned w;
         __builtin_memcpy(&w, &v, 4);
         __builtin_nontemporal_store(w, reinterpret_cast<unsigned *>(p));
@@ -237,6 +243,76 @@ template <> struct Pix<1> {           // RGBA32F
         st_stream<float4>(base, i * 16u, make_float4(r, g, b, 1.0f));
     }
 };
+// RGBA16F: linear half floats, as the reference camera's HDR render target
+// (ARGBHalf: Assets/Scenes/SampleScene.unity:663 m_HDR, linear colour space
+// ProjectSettings/ProjectSettings.asset:50) hands them to OnRenderImage
+// (.cs:101).  Values above 1 pass unclipped up to the reference's saturate
+// (YIQToRGB.shader); the output is rounded to half (round to nearest even).
+template <> struct Pix<2> {
+    static constexpr int bpp = 8;
+    using raw_t = uint2;
+    __device__ static raw_t raw(const uint8_t *base, size_t i)
+    {
+        return reinterpret_cast<const uint2 *>(base)[i];
+    }
+    __device__ static float h2f(unsigned bits)
+    {
+        return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
+    }
+    __device__ static unsigned f2h(float v)
+    {
+        return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)v);
+    }
+    __device__ static float4 cvt(raw_t u)
+    {
+        return make_float4(h2f(u.x), h2f(u.x >> 16), h2f(u.y), h2f(u.y >> 16));
+    }
+    __device__ static uint2 pack(float r, float g, float b)
+    {
+        return make_uint2(f2h(r) | f2h(g) << 16, f2h(b) | 0x3C00u << 16);   // alpha 1.0
+    }
+    __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
+    {
+        st_stream<uint2>(base, i * 8u, pack(r, g, b));
+    }
+};
+// RGBA8 sRGB: an 8-bit sRGB render target under Unity's Linear colour space
+// is sampled as linear light and encoded on write, so the pipeline sees
+// linear values.  Decode: the exact 256-entry table (tools/gen_srgb.py);
+// encode of a saturated value: 255 srgb(v) rounded, found from the pow
+// approximation and corrected by one step against the exact thresholds
+// kSrgbThr (the approximation is within one code of the exact one).
+template <> struct Pix<3> {
+    static constexpr int bpp = 4;
+    using raw_t = uint32_t;
+    __device__ static raw_t raw(const uint8_t *base, size_t i)
+    {
+        return reinterpret_cast<const uint32_t *>(base)[i];
+    }
+    __device__ static float4 cvt(raw_t u)
+    {
+        return make_float4(kSrgbDec[u & 255u], kSrgbDec[(u >> 8) & 255u], kSrgbDec[(u >> 16) & 255u],
+                           (float)(u >> 24) * (1.0f / 255.0f));
+    }
+    __device__ static uint32_t enc(float v)
+    {
+        const float s = v <= 0.0031308f ? 12.92f * v : 1.055f * __powf(v, 1.0f / 2.4f) - 0.055f;
+        int b = min(max((int)(s * 255.0f + 0.5f), 0), 255);
+        b += v >= kSrgbThr[b + 1] ? 1 : 0;
+        b -= v < kSrgbThr[b] ? 1 : 0;
+        return (uint32_t)b;
+    }
+    __device__ static uint32_t pack(float r, float g, float b)
+    {
+        return enc(r) | (enc(g) << 8) | (enc(b) << 16) | (255u << 24);
+    }
+    __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
+    {
+        st_stream<uint32_t>(base, i * 4u, pack(r, g, b));
+    }
+};
+// saturated before the store: the UNORM destinations (RGBA8, RGBA8 sRGB)
+template <int FMT> constexpr bool kUnorm = FMT == 0 || FMT == 3;
 
 // RGBToYIQ.shader:46-50 rows
 __device__ __forceinline__ float luma(float4 c) { return 0.299f * c.x + 0.587f * c.y + 0.114f * c.z; }
@@ -257,7 +333,7 @@ __device__ __forceinline__ float luma_units(typename Pix<FMT>::raw_t u)
         const unsigned hi = __builtin_amdgcn_udot4(u, 0x00000201u, 0u, false);    // R + 2 G
         return (float)__builtin_amdgcn_udot4(u, 0x00724B2Bu, hi << 8, false);   // + 43 R + 75 G + 114 B
     } else {
-        return luma(u);
+        return luma(Pix<FMT>::cvt(u));
     }
 }
 
@@ -272,7 +348,8 @@ __device__ __forceinline__ float2 chroma_iq(typename Pix<FMT>::raw_t u)
         return make_float2((0.596f * k) * r + (-0.274f * k) * gg + (-0.322f * k) * b,
                            (0.211f * k) * r + (-0.523f * k) * gg + (0.312f * k) * b);
     } else {
-        return make_float2(chroma_i(u), chroma_q(u));
+        const float4 c = Pix<FMT>::cvt(u);
+        return make_float2(chroma_i(c), chroma_q(c));
     }
 }
 
@@ -289,7 +366,8 @@ __device__ __forceinline__ c2 chroma_iq2(typename Pix<FMT>::raw_t u)
         const float r = (float)(u & 255u), gg = (float)((u >> 8) & 255u), b = (float)((u >> 16) & 255u);
         return mk(0.596f * k, 0.211f * k) * r + mk(-0.274f * k, -0.523f * k) * gg + mk(-0.322f * k, 0.312f * k) * b;
     } else {
-        return mk(0.596f, 0.211f) * u.x + mk(-0.274f, -0.523f) * u.y + mk(-0.322f, 0.312f) * u.z;
+        const float4 c = Pix<FMT>::cvt(u);
+        return mk(0.596f, 0.211f) * c.x + mk(-0.274f, -0.523f) * c.y + mk(-0.322f, 0.312f) * c.z;
     }
 }
 
@@ -347,9 +425,9 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
 #pragma unroll
         for (int j = 0; j < 8; ++j) cw[j] = colW3[min(max(t + j * T - g.x0, 0), g.W - 1)];
     }
-    // RGBA8: all 32 pixel loads of the thread in one batch; RGBA32F (4x the
-    // registers): two batches of 16
-    constexpr int UB = FMT == 0 ? 8 : 4;
+    // RGBA8 / RGBA16F: all 32 pixel loads of the thread in one batch; RGBA32F
+    // (4x the registers of RGBA8): two batches of 16
+    constexpr int UB = BPP == 16 ? 4 : 8;
     if constexpr (GEN) {
         if (valid) {
             Tap4 ta = rowT[ra];
@@ -2057,7 +2135,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         const unsigned base = (unsigned)(row * g.W);
         raw_t p[6];
         p[0] = ld_off<raw_t>(img, (base + cl) * bpp);
-        if constexpr (FMT == 0) {
+        if constexpr (bpp == 4) {
             const uint4 m = ld_off<uint4>(img, (base + (unsigned)X) * bpp);
             p[1] = m.x; p[2] = m.y; p[3] = m.z; p[4] = m.w;
         } else {
@@ -2190,16 +2268,16 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
                         yiq_rgb(yb, cc, rr[k], gg[k], bb[k]);
                     }
                     const unsigned o = (unsigned)(i * g.W + X);
-                    if constexpr (FMT == 0) {
+                    if constexpr (bpp == 4) {
                         uint4 px;
-                        px.x = Pix<0>::pack(rr[0], gg[0], bb[0]);
-                        px.y = Pix<0>::pack(rr[1], gg[1], bb[1]);
-                        px.z = Pix<0>::pack(rr[2], gg[2], bb[2]);
-                        px.w = Pix<0>::pack(rr[3], gg[3], bb[3]);
+                        px.x = Pix<FMT>::pack(rr[0], gg[0], bb[0]);
+                        px.y = Pix<FMT>::pack(rr[1], gg[1], bb[1]);
+                        px.z = Pix<FMT>::pack(rr[2], gg[2], bb[2]);
+                        px.w = Pix<FMT>::pack(rr[3], gg[3], bb[3]);
                         st_stream<uint4>(outp, o * 4u, px);
                     } else {
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) Pix<1>::store(outp, o + k, rr[k], gg[k], bb[k]);
+                        for (int k = 0; k < 4; ++k) Pix<FMT>::store(outp, o + k, rr[k], gg[k], bb[k]);
                     }
                 }
             }
@@ -2305,7 +2383,7 @@ void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
         const unsigned base = (unsigned)(row * g.W);
         raw_t p[6];
         p[0] = ld_off<raw_t>(img, (base + cl) * bpp);
-        if constexpr (FMT == 0) {
+        if constexpr (bpp == 4) {
             const uint4 m = ld_off<uint4>(img, (base + (unsigned)X) * bpp);
             p[1] = m.x; p[2] = m.y; p[3] = m.z; p[4] = m.w;
         } else {
@@ -2352,16 +2430,16 @@ void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
                 yiq_rgb(yb, cc, rr[k], gg[k], bb[k]);
             }
             const unsigned o = (unsigned)(i * g.W + X);
-            if constexpr (FMT == 0) {
+            if constexpr (bpp == 4) {
                 uint4 px;
-                px.x = Pix<0>::pack(rr[0], gg[0], bb[0]);
-                px.y = Pix<0>::pack(rr[1], gg[1], bb[1]);
-                px.z = Pix<0>::pack(rr[2], gg[2], bb[2]);
-                px.w = Pix<0>::pack(rr[3], gg[3], bb[3]);
+                px.x = Pix<FMT>::pack(rr[0], gg[0], bb[0]);
+                px.y = Pix<FMT>::pack(rr[1], gg[1], bb[1]);
+                px.z = Pix<FMT>::pack(rr[2], gg[2], bb[2]);
+                px.w = Pix<FMT>::pack(rr[3], gg[3], bb[3]);
                 st_stream<uint4>(outp, o * 4u, px);
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) Pix<1>::store(outp, o + k, rr[k], gg[k], bb[k]);
+                for (int k = 0; k < 4; ++k) Pix<FMT>::store(outp, o + k, rr[k], gg[k], bb[k]);
             }
         }
     }
@@ -2512,7 +2590,7 @@ void k_dbg_out(const float *__restrict__ tex, size_t tex_stride, uint8_t *__rest
     } else {
         v = (show_mag ? mag : pha)[(size_t)(g.y0 + Y) * g.N + g.x0 + X];
     }
-    if (FMT == 0) v = sat(v);   // UNORM destination
+    if (kUnorm<FMT>) v = sat(v);   // UNORM destination
     Pix<FMT>::store(frames_out + (size_t)(frame0 + k) * frame_bytes, (unsigned)p, v, 0.0f, 0.0f);
 }
 

@@ -9,7 +9,11 @@
  * output read back through the exporter's mapping must be bitwise the output
  * of the same stream processed from ordinary device buffers.
  *
- *   mm_extmem_check [-w W] [-h H] [-n frames]    -> prints "extmem ok ..." / exits 1
+ *   mm_extmem_check [-w W] [-h H] [-n frames] [-f format]
+ *                                                 -> prints "extmem ok ..." / exits 1
+ * format: the mm.h code (0 RGBA8, 1 RGBA32F, 2 RGBA16F: the engine's HDR
+ * target, with values up to 1.5; 3 RGBA8_SRGB): the synthetic RGBA8 stream
+ * converted on the host.
  */
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
@@ -66,19 +70,63 @@ static int export_alloc(size_t bytes, exported *x)
     return 0;
 }
 
+/* binary16 bits of a float in [0, 65504) (round to nearest even; no
+ * subnormals arise from the synthetic stream's values) */
+static unsigned short half_bits(float f)
+{
+    unsigned x;
+    memcpy(&x, &f, 4);
+    if (f == 0.0f) return 0;
+    unsigned h = ((((x >> 23) & 0xffu) - 127 + 15) << 10) | ((x & 0x7fffffu) >> 13);
+    const unsigned rem = x & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+    return (unsigned short)h;
+}
+
+/* the synthetic RGBA8 stream as frames of `format` (host memory) */
+static void *host_frames(int W, int H, int n, int format, size_t bytes)
+{
+    const size_t px = (size_t)W * H * 4 * n;
+    unsigned char *u8 = (unsigned char *)malloc(px);
+    void *d = NULL;
+    if (!u8 || hipMalloc(&d, px) != hipSuccess) return NULL;
+    if (mm_synth_frames(d, W, H, 0, n, 0x5EED0000ull, 0, NULL) != MM_OK ||
+        hipMemcpy(u8, d, px, hipMemcpyDeviceToHost) != hipSuccess)
+        return NULL;
+    hipFree(d);
+    if (format == MM_RGBA8 || format == MM_RGBA8_SRGB) return u8;
+    void *out = malloc(bytes);
+    if (!out) return NULL;
+    for (size_t i = 0; i < px; ++i) {
+        const float v = (float)u8[i] / 255.0f;
+        if (format == MM_RGBA32F) ((float *)out)[i] = v;
+        else ((unsigned short *)out)[i] = half_bits((i & 3) == 3 ? 1.0f : 1.5f * v);
+    }
+    free(u8);
+    return out;
+}
+
 int main(int argc, char **argv)
 {
-    int W = 256, H = 144, n = 8;
+    int W = 256, H = 144, n = 8, format = MM_RGBA8;
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "-w")) W = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "-h")) H = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "-n")) n = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "-f")) format = atoi(argv[i + 1]);
     }
-    const size_t fb = (size_t)W * H * 4, bytes = fb * (size_t)n;
+    size_t fb = 0;
+    MCHECK(mm_frame_bytes(W, H, format, &fb));
+    const size_t bytes = fb * (size_t)n;
     HCHECK(hipSetDevice(0));
+    void *src = host_frames(W, H, n, format, bytes);
+    if (!src) {
+        fprintf(stderr, "host frames failed\n");
+        return 1;
+    }
     exported xin, xout;
     if (export_alloc(bytes, &xin) || export_alloc(bytes, &xout)) return 1;
-    MCHECK(mm_synth_frames(xin.va, W, H, 0, n, 0x5EED0000ull, 0, NULL));
+    HCHECK(hipMemcpy(xin.va, src, bytes, hipMemcpyHostToDevice));   /* the engine renders */
     HCHECK(hipMemset(xout.va, 0, xout.size));
     HCHECK(hipDeviceSynchronize());
 
@@ -97,7 +145,7 @@ int main(int argc, char **argv)
     }
     for (int k = 0; k < n; ++k)   /* the reference's pattern: one call per frame */
         MCHECK(mm_process(ha, (const char *)mm_ext_frames_ptr(in) + fb * k,
-                          (char *)mm_ext_frames_ptr(out) + fb * k, MM_RGBA8, MM_FRAMES_ON_DEVICE, NULL));
+                          (char *)mm_ext_frames_ptr(out) + fb * k, format, MM_FRAMES_ON_DEVICE, NULL));
     HCHECK(hipDeviceSynchronize());
 
     /* the same stream from ordinary device buffers */
@@ -106,8 +154,8 @@ int main(int argc, char **argv)
     void *din = NULL, *dout = NULL;
     HCHECK(hipMalloc(&din, bytes));
     HCHECK(hipMalloc(&dout, bytes));
-    MCHECK(mm_synth_frames(din, W, H, 0, n, 0x5EED0000ull, 0, NULL));
-    MCHECK(mm_process_stream(hb, din, dout, n, MM_RGBA8, NULL));
+    HCHECK(hipMemcpy(din, src, bytes, hipMemcpyHostToDevice));
+    MCHECK(mm_process_stream(hb, din, dout, n, format, NULL));
     HCHECK(hipDeviceSynchronize());
 
     unsigned char *a = (unsigned char *)malloc(bytes), *b = (unsigned char *)malloc(bytes);
@@ -132,7 +180,8 @@ int main(int argc, char **argv)
         fprintf(stderr, "extmem: %zu of %zu bytes differ\n", diff, bytes);
         return 1;
     }
-    printf("extmem ok: %dx%d x %d frames, zero-copy output == device-buffer output (byte sum %llu)\n",
-           W, H, n, sum);
+    free(src);
+    printf("extmem ok: %dx%d x %d frames, format %d, zero-copy output == device-buffer output "
+           "(byte sum %llu)\n", W, H, n, format, sum);
     return 0;
 }

@@ -7,9 +7,12 @@
  * shift of step s+1 is posted on the ring's own stream before step s's frames
  * are processed, so the transfer runs under step s's kernels.
  */
+#define _GNU_SOURCE   /* dladdr */
 #include "mm_ring.h"
 #include "mm_ring_local.h"
 
+#include <dlfcn.h>
+#include <math.h>
 #include <pthread.h>
 
 #include <rccl/rccl.h>
@@ -124,8 +127,9 @@ static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int wid
 {
     if (!out) return MM_ERR_INVALID;
     *out = NULL;
+    size_t fbytes = 0;
     if (!h || world < 1 || rank < 0 || rank >= world || chunk < 1 || width < 1 || height < 1 ||
-        (format != MM_RGBA8 && format != MM_RGBA32F))
+        mm_frame_bytes(width, height, format, &fbytes) != MM_OK)
         return MM_ERR_INVALID;
     mm_params p;
     int rc = mm_get_params(h, &p);
@@ -139,7 +143,7 @@ static int ring_alloc(int world, int rank, int hip_device, mm_handle *h, int wid
     r->format = format;
     r->h = h;
     r->posted[0] = r->posted[1] = -1;
-    r->frame_bytes = (size_t)width * height * (format == MM_RGBA8 ? 4 : 16);
+    r->frame_bytes = fbytes;
     /* the IIR state is a history of frames, not one frame's function: nothing
      * is shifted, each rank warms its filter on a halo (mm_ring_step_halo) */
     r->halo_mode = p.mode == MM_MODE_STEERABLE && p.temporal_filter == MM_FILTER_IIR;
@@ -383,13 +387,18 @@ int mm_ring_halo_frames(const mm_ring *r, int *frames)
     if (rc) return rc;
     /* the slower pole (1 - iir_low) decays below 1e-6 of its start value:
      * ceil(ln 1e-6 / ln(1 - iir_low)); 270 frames at the default 0.05 */
-    const double d = 1.0 - (double)p.iir_low;
-    int k = 1;
-    double a = d;
-    while (a > 1e-6 && k < 100000) {
-        a *= d;
-        ++k;
-    }
-    *frames = k;
+    const double k = ceil(log(1e-6) / log1p(-(double)p.iir_low));
+    if (!(k <= MM_RING_HALO_MAX)) return MM_ERR_UNSUPPORTED;   /* iir_low below ~0.0067 */
+    *frames = k < 1.0 ? 1 : (int)k;
     return MM_OK;
+}
+
+/* The libmm355 this library's mm_* calls resolve to (dladdr of the bound
+ * mm_process_stream): a caller that loaded another build of the operator
+ * (an A/B variant) checks that both libraries are the same one. */
+const char *mm_ring_core_library(void)
+{
+    Dl_info info;
+    if (dladdr((void *)&mm_process_stream, &info) && info.dli_fname) return info.dli_fname;
+    return NULL;
 }

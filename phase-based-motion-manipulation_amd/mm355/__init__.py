@@ -16,7 +16,8 @@ finds the same names, argument meaning and error behaviour:
 There is no CPU fallback.  If the library or a gfx950 device is missing,
 construction/Start raises ``MMError`` — loudly, never silently.
 """
-from .binding import (MMError, lib, load_library, LIB_PATH, RGBA8, RGBA32F,
+from .binding import (MMError, lib, load_library, LIB_PATH, RGBA8, RGBA32F, RGBA16F, RGBA8_SRGB,
+                      FORMAT_BPP, frame_bytes,
                       EDGE_REPEAT, EDGE_CLAMP, MODE_PYRAMID, MODE_STANDARD, MODE_STEERABLE,
                       FILTER_DIFF, FILTER_IIR, Params, Handle,
                       abi_symbols, resample_table, strerror)
@@ -24,7 +25,8 @@ from .processor import MotionMagnificationProcessor
 from .stream import ShardedStream, shard_range
 from .ring import Ring, new_ring_id, ring_lib
 
-__all__ = ["MMError", "lib", "load_library", "LIB_PATH", "RGBA8", "RGBA32F",
+__all__ = ["MMError", "lib", "load_library", "LIB_PATH", "RGBA8", "RGBA32F", "RGBA16F",
+           "RGBA8_SRGB", "FORMAT_BPP", "frame_bytes",
            "EDGE_REPEAT", "EDGE_CLAMP", "MODE_PYRAMID", "MODE_STANDARD", "MODE_STEERABLE",
            "FILTER_DIFF", "FILTER_IIR", "Params", "Handle", "abi_symbols",
            "resample_table", "strerror", "MotionMagnificationProcessor",

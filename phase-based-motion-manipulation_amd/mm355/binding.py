@@ -12,6 +12,9 @@ HEADER = os.path.join(REPO_ROOT, "include", "mm.h")
 
 RGBA8 = 0
 RGBA32F = 1
+RGBA16F = 2         # linear half (the reference camera's HDR target), ABI 10
+RGBA8_SRGB = 3      # 8-bit sRGB target in Linear colour space, ABI 10
+FORMAT_BPP = {RGBA8: 4, RGBA32F: 16, RGBA16F: 8, RGBA8_SRGB: 4}
 EDGE_REPEAT = 0
 EDGE_CLAMP = 1
 MODE_PYRAMID = 0
@@ -75,13 +78,14 @@ class Params(ctypes.Structure):
 
 
 _lib = None
-ABI_VERSION = 9   # include/mm.h MM_ABI_VERSION
+_lib_path = None
+ABI_VERSION = 10  # include/mm.h MM_ABI_VERSION
 
 
 def load_library(path=None):
     """Load the HIP product library; raises if it is missing (no fallback).
     MM355_LIB overrides the path (A/B builds of the same library)."""
-    global _lib
+    global _lib, _lib_path
     if _lib is not None:
         return _lib
     path = path or os.environ.get("MM355_LIB") or LIB_PATH
@@ -98,6 +102,7 @@ def load_library(path=None):
         "mm_set_params": (ci, [vp, pp]),
         "mm_get_params": (ci, [vp, pp]),
         "mm_padded_size": (ci, [vp, ctypes.POINTER(ci)]),
+        "mm_frame_bytes": (ci, [ci, ci, ci, ctypes.POINTER(sz)]),
         "mm_process": (ci, [vp, vp, vp, ci, ci, vp]),
         "mm_process_stream": (ci, [vp, vp, vp, ci, ci, vp]),
         "mm_reset": (ci, [vp]),
@@ -125,6 +130,8 @@ def load_library(path=None):
             continue
         if abi < 6 and name in ("mm_import_frames", "mm_ext_frames_ptr", "mm_release_frames"):
             continue
+        if abi < 10 and name == "mm_frame_bytes":
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -133,7 +140,14 @@ def load_library(path=None):
     if abi > ABI_VERSION or abi < 2:
         raise MMError(-1, f"{path}: ABI {abi}, binding expects <= {ABI_VERSION}")
     _lib = L
+    _lib_path = os.path.realpath(path)
     return L
+
+
+def library_path():
+    """Real path of the libmm355 build this process loaded (MM355_LIB or the tree's)."""
+    load_library()
+    return _lib_path
 
 
 def lib():
@@ -154,6 +168,13 @@ def abi_symbols():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(mm_[a-z_0-9]+)\s*\(", txt)))
+
+
+def frame_bytes(width, height, fmt):
+    """mm_frame_bytes: bytes of one W x H frame of `fmt`."""
+    n = ctypes.c_size_t()
+    check(lib().mm_frame_bytes(width, height, fmt, ctypes.byref(n)), "mm_frame_bytes")
+    return n.value
 
 
 def resample_table(width, height, axis, edge_mode=EDGE_REPEAT):

@@ -7,16 +7,20 @@ snake_case; methods keep the reference's Unity callback names.
 import numpy as np
 
 from .binding import (EDGE_REPEAT, FILTER_DIFF, MODE_PYRAMID, MODE_STANDARD, MODE_STEERABLE,
-                      RGBA8, RGBA32F, Handle, MMError, Params)
+                      RGBA8, RGBA8_SRGB, RGBA16F, RGBA32F, Handle, MMError, Params)
 
 
-def _fmt_of(frame):
+def _fmt_of(frame, srgb=False):
+    """Frame format from the dtype: uint8 UNORM (or sRGB-encoded with srgb),
+    float16 (linear half, the HDR camera target), float32."""
     dt = str(getattr(frame, "dtype", ""))
     if dt.endswith("uint8"):
-        return RGBA8
+        return RGBA8_SRGB if srgb else RGBA8
+    if dt.endswith("float16"):
+        return RGBA16F
     if dt.endswith("float32"):
         return RGBA32F
-    raise MMError(-1, f"frame dtype {dt} (want uint8 or float32 RGBA)")
+    raise MMError(-1, f"frame dtype {dt} (want uint8, float16 or float32 RGBA)")
 
 
 def _is_device(frame):
@@ -37,8 +41,12 @@ class MotionMagnificationProcessor:
                  low_frequency_cutoff=0.05, high_frequency_cutoff=0.4, filter_steepness=3.0,
                  motion_sensitivity=1.5, enhance_edges=True, edge_enhancement=0.8,
                  edge_mode=EDGE_REPEAT, orientations=1, temporal_filter=FILTER_DIFF,
-                 iir_low=None, iir_high=None, device=0):
+                 iir_low=None, iir_high=None, srgb=False, device=0):
         self.width, self.height, self.device = width, height, device
+        # 8-bit frames are sRGB-encoded render targets under Unity's Linear colour
+        # space (ProjectSettings/ProjectSettings.asset:50): decoded to linear light
+        # on read and encoded on write (MM_RGBA8_SRGB); False: UNORM bytes
+        self.srgb = srgb
         self.apply_motion_magnification = apply_motion_magnification  # .cs:12
         self.show_magnitude = show_magnitude                          # .cs:13
         self.show_phase = show_phase                                  # .cs:14
@@ -104,14 +112,14 @@ class MotionMagnificationProcessor:
             self._handle.set_params(self._params())
 
     def OnRenderImage(self, source, destination):
-        """OnRenderImage (.cs:101-143). source/destination: [H, W, 4] uint8 or
-        float32, both torch CUDA tensors (async on torch's current stream) or
-        both host numpy arrays (synchronous)."""
+        """OnRenderImage (.cs:101-143). source/destination: [H, W, 4] uint8,
+        float16 or float32, both torch CUDA tensors (async on torch's current
+        stream) or both host numpy arrays (synchronous)."""
         if self._handle is None:                       # !isInitialized -> Blit (.cs:103-107)
             destination[...] = source
             return
-        fmt = _fmt_of(source)
-        if _fmt_of(destination) != fmt:
+        fmt = _fmt_of(source, self.srgb)
+        if _fmt_of(destination, self.srgb) != fmt:
             raise MMError(-1, "source/destination formats differ")
         on_dev = _is_device(source)
         if on_dev != _is_device(destination):
@@ -148,4 +156,5 @@ class MotionMagnificationProcessor:
 
 
 def host_frames(n, h, w, fmt):
-    return np.zeros((n, h, w, 4), np.uint8 if fmt == RGBA8 else np.float32)
+    dt = {RGBA8: np.uint8, RGBA8_SRGB: np.uint8, RGBA16F: np.float16}.get(fmt, np.float32)
+    return np.zeros((n, h, w, 4), dt)

@@ -9,24 +9,49 @@ torch.distributed process group) and calls mm_ring_step per step.
 import ctypes
 import os
 
-from .binding import MMError, PKG_DIR, _ptr, lib as _mm_lib
+from .binding import MMError, PKG_DIR, _ptr, library_path
 
 RING_LIB_PATH = os.path.join(PKG_DIR, "lib", "libmm_ring.so")
+
+
+def ring_lib_path(core=None):
+    """The ring library that belongs to the libmm355 build `core` (default: the
+    one this process loaded): MM355_RING_LIB, else beside it — libmm_ring.so
+    next to libmm355.so, <name>_ring.so next to an A/B variant <name>.so
+    (scripts/build_variants.sh builds both, the ring linked to its variant)."""
+    if os.environ.get("MM355_RING_LIB"):
+        return os.environ["MM355_RING_LIB"]
+    core = core or library_path()
+    d, b = os.path.split(core)
+    if b == "libmm355.so":
+        return os.path.join(d, "libmm_ring.so")
+    return os.path.join(d, os.path.splitext(b)[0] + "_ring.so")
 ID_BYTES = 128   # MM_RING_ID_BYTES == NCCL_UNIQUE_ID_BYTES
 
 _rl = None
 
 
 def ring_lib():
-    """Load libmm_ring.so (after libmm355.so, which it links); raises if the
-    library is not built (no fallback to another transport)."""
+    """Load the ring library of the loaded libmm355 build (ring_lib_path);
+    raises if it is not built (no fallback to another transport) or if its
+    mm_* calls resolve to another libmm355 than the one this process loaded
+    (two builds mixed in one process: the ring would run the other build's
+    kernels on this build's handles)."""
     global _rl
     if _rl is not None:
         return _rl
-    _mm_lib()
-    if not os.path.exists(RING_LIB_PATH):
-        raise MMError(-3, f"ring library not built: {RING_LIB_PATH} (run __graft_entry__.build())")
-    L = ctypes.CDLL(RING_LIB_PATH)
+    core = library_path()
+    path = ring_lib_path(core)
+    if not os.path.exists(path):
+        raise MMError(-3, f"ring library not built: {path} (run __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    L.mm_ring_core_library.restype = ctypes.c_char_p
+    L.mm_ring_core_library.argtypes = []
+    bound = L.mm_ring_core_library()
+    bound = os.path.realpath(bound.decode()) if bound else None
+    if bound != core:
+        raise MMError(-1, f"{path} is bound to {bound}, but this process loaded {core}: "
+                          "load the ring library built with that libmm355 (MM355_RING_LIB)")
     vp, ci = ctypes.c_void_p, ctypes.c_int
     for name, res, args in (
             ("mm_ring_get_id", ci, [ctypes.c_char_p]),

@@ -63,7 +63,8 @@ typedef struct interop {
     mm_handle *h;
     VkDevice dev;
     VkQueue queue;
-    VkBuffer buf[2];                 /* 0: input frame, 1: output frame (linear RGBA8) */
+    VkBuffer buf[2];                 /* 0: input frame, 1: output frame (tightly packed texels,
+                                        sized for the widest format, 16 B/px) */
     VkDeviceMemory mem[2];
     mm_ext_frames *ext[2];           /* the same memory as HIP device pointers */
     size_t frame_bytes;
@@ -82,8 +83,10 @@ typedef struct interop {
 
 /* Host waits on the timeline are bounded: a chain that cannot complete (a
  * device lost, a failed leg the repair below could not close) must not hang
- * Unity's render thread. */
+ * Unity's render thread.  A timeout is retried (a slow frame is not a lost
+ * device) up to MM_UNITY_WAIT_TRIES times before the interop gives up. */
 #define MM_UNITY_WAIT_NS 2000000000ull
+#define MM_UNITY_WAIT_TRIES 5
 
 static IUnityInterfaces *s_unity;
 static IUnityGraphics *s_graphics;
@@ -184,7 +187,7 @@ UNITY_INTERFACE_EXPORT int UNITY_INTERFACE_API mm_unity_create(int width, int he
     s_io.dev = vi.device;
     s_io.queue = vi.graphicsQueue;
     s_io.stream = (hipStream_t)mm_stream(s_io.h);
-    s_io.frame_bytes = (size_t)width * height * 4;
+    s_io.frame_bytes = (size_t)width * height * 16;   /* any format (unity_frame_format) fits */
     if ((rc = make_shared_buffer(&vi, s_io.frame_bytes, 0)) || (rc = make_shared_buffer(&vi, s_io.frame_bytes, 1)) ||
         (rc = make_shared_semaphore(&vi)) || (rc = make_command_buffers(&vi))) {
         mm_unity_destroy(s_io.h);
@@ -249,10 +252,31 @@ static int submit(VkCommandBuffer cb, uint64_t wait, uint64_t signal)
     return vkQueueSubmit(s_io.queue, 1, &si, VK_NULL_HANDLE) == VK_SUCCESS;
 }
 
-static int host_wait(uint64_t value)
+/* VK_SUCCESS, VK_TIMEOUT after MM_UNITY_WAIT_TRIES bounded waits, or the
+ * error (VK_ERROR_DEVICE_LOST) */
+static VkResult host_wait_result(uint64_t value)
 {
     VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &value};
-    return s_io.wait_sem(s_io.dev, &wi, MM_UNITY_WAIT_NS) == VK_SUCCESS;
+    VkResult r = VK_TIMEOUT;
+    for (int k = 0; k < MM_UNITY_WAIT_TRIES && r == VK_TIMEOUT; ++k) r = s_io.wait_sem(s_io.dev, &wi, MM_UNITY_WAIT_NS);
+    return r;
+}
+
+static int host_wait(uint64_t value) { return host_wait_result(value) == VK_SUCCESS; }
+
+/* include/mm.h frame format of a render target's texels (the reference
+ * camera's HDR target is R16G16B16A16_SFLOAT, an LDR one R8G8B8A8_SRGB under
+ * Linear colour space); -1: not one the operator takes (BGRA orders
+ * included), so the event falls back to the passthrough Blit. */
+static int unity_frame_format(VkFormat f)
+{
+    switch (f) {
+    case VK_FORMAT_R8G8B8A8_UNORM: return MM_RGBA8;
+    case VK_FORMAT_R8G8B8A8_SRGB: return MM_RGBA8_SRGB;
+    case VK_FORMAT_R16G16B16A16_SFLOAT: return MM_RGBA16F;
+    case VK_FORMAT_R32G32B32A32_SFLOAT: return MM_RGBA32F;
+    default: return -1;
+    }
 }
 
 static int host_signal(uint64_t value)
@@ -287,6 +311,13 @@ static void UNITY_INTERFACE_API on_render_event(int event_id, void *data)
         !s_vulkan->AccessTexture(f->destination, &sub, VK_IMAGE_LAYOUT_UNDEFINED, 0, 0,
                                  kUnityVulkanResourceAccess_ObserveOnly, &dst))
         return;
+    /* source and destination share the camera's format (Blit(source,
+     * destination) of the reference keeps it); the interop buffers hold any */
+    const int fmt = unity_frame_format(src.format);
+    if (fmt < 0 || unity_frame_format(dst.format) != fmt) {
+        s_io.broken = 1;   /* C# Blits (mm_unity_event_ok) */
+        return;
+    }
     const uint64_t i = s_io.frame, base = 3 * i;
     const int set = (int)(i & 1);
     /* the set's command buffers were last submitted for frame i-2 */
@@ -311,8 +342,10 @@ static void UNITY_INTERFACE_API on_render_event(int event_id, void *data)
         return;
     }
     void *in = mm_ext_frames_ptr(s_io.ext[0]), *out = mm_ext_frames_ptr(s_io.ext[1]);
-    if (mm_process(f->h, in, out, MM_RGBA8, MM_FRAMES_ON_DEVICE, s_io.stream) != MM_OK &&
-        hipMemcpyAsync(out, in, s_io.frame_bytes, hipMemcpyDeviceToDevice, s_io.stream) != hipSuccess) {   /* .cs:105 */
+    size_t fb = 0;
+    (void)mm_frame_bytes(f->width, f->height, fmt, &fb);
+    if (mm_process(f->h, in, out, fmt, MM_FRAMES_ON_DEVICE, s_io.stream) != MM_OK &&
+        hipMemcpyAsync(out, in, fb, hipMemcpyDeviceToDevice, s_io.stream) != hipSuccess) {   /* .cs:105 */
         (void)hipStreamSynchronize(s_io.stream);
         close_chain(base + 1, base);
         return;
@@ -347,21 +380,25 @@ UNITY_INTERFACE_EXPORT UnityRenderingEventAndData UNITY_INTERFACE_API mm_unity_e
 }
 
 /* OnDestroy -> ReleaseResources (.cs:96-99): waits for the last frame's chain,
- * then releases in reverse order of creation (safe on a partial create). */
+ * then releases in reverse order of creation (safe on a partial create).  The
+ * Vulkan objects are freed only once the chain is known to be done (the wait
+ * returned VK_SUCCESS) or can never run again (VK_ERROR_DEVICE_LOST); if it
+ * is still pending after the retried waits, a queued copy may still use the
+ * buffers, their memory and the semaphore, so they are leaked instead. */
 UNITY_INTERFACE_EXPORT void UNITY_INTERFACE_API mm_unity_destroy(mm_handle *h)
 {
     if (!h || h != s_io.h) return;
+    int vk_free = 1;
     if (s_io.frame && s_io.wait_sem) {
-        const uint64_t last = 3 * s_io.frame;
-        VkSemaphoreWaitInfo wi = {VK_STRUCTURE_TYPE_SEMAPHORE_WAIT_INFO, NULL, 0, 1, &s_io.sem, &last};
-        (void)s_io.wait_sem(s_io.dev, &wi, MM_UNITY_WAIT_NS);
+        const VkResult r = host_wait_result(3 * s_io.frame);
+        vk_free = r == VK_SUCCESS || r == VK_ERROR_DEVICE_LOST;
     }
     if (s_io.stream) (void)hipStreamSynchronize(s_io.stream);
     for (int k = 0; k < 2; ++k)
         if (s_io.ext[k]) mm_release_frames(s_io.ext[k]);
     if (s_io.hsem) (void)hipDestroyExternalSemaphore(s_io.hsem);
     mm_destroy(h);
-    if (s_io.dev) {
+    if (s_io.dev && vk_free) {
         if (s_io.pool) vkDestroyCommandPool(s_io.dev, s_io.pool, NULL);   /* frees the command buffers */
         for (int k = 0; k < 2; ++k) {
             if (s_io.buf[k]) vkDestroyBuffer(s_io.dev, s_io.buf[k], NULL);

@@ -14,6 +14,11 @@ while [ $# -gt 0 ]; do
     done
     wait
     /opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 -shared -o lib/variants/$n.so $o/*.o
+    # the variant's own ring library (mm355/ring.py refuses a ring bound to
+    # another libmm355 than the one MM355_LIB loaded)
+    gcc -O2 -std=gnu11 -fPIC -shared -I../include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+      -o lib/variants/${n}_ring.so host/mm_ring.c -Llib/variants -l:$n.so -L/opt/rocm/lib -lrccl \
+      -lamdhip64 -lpthread -ldl -lm -Wl,-rpath,'$ORIGIN' -Wl,-rpath,/opt/rocm/lib
   ) &
 done
 wait

@@ -40,19 +40,26 @@ def oracle_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, app
 
 
 def gpu_run(W, H, frames, levels=5, S=10.0, edge=0, minf=0.05, maxf=0.45, mode="frame",
-            apply=True, standard=None, debug=None, batch=8):
+            apply=True, standard=None, debug=None, batch=8, fmt=None, extra=None):
     """batch: mm_set_batch frames per internal batch (8: multi-frame streams
-    cross batch boundaries, where K2's state is stored and reloaded)."""
+    cross batch boundaries, where K2's state is stored and reloaded).
+    fmt: the frame format (default from the dtype: uint8 RGBA8, float16
+    RGBA16F, float32 RGBA32F; RGBA8_SRGB must be named).  extra: more
+    mm_params fields."""
     import torch
     import mm355
-    extra = {} if standard is None else dict(mode=mm355.MODE_STANDARD, **_std_fields(standard))
+    extra = dict(extra or {})
+    if standard is not None:
+        extra.update(mode=mm355.MODE_STANDARD, **_std_fields(standard))
     if debug is not None:
         extra.update(show_magnitude=debug[0], show_phase=debug[1])
     p = mm355.Params.make(levels=levels, min_freq=minf, max_freq=maxf, phase_scale=S,
                           edge_mode=edge, apply_magnification=apply, **extra)
     h = mm355.Handle(W, H, p)
     h.set_batch(batch)
-    fmt = mm355.RGBA8 if frames[0].dtype == np.uint8 else mm355.RGBA32F
+    if fmt is None:
+        fmt = {np.dtype(np.uint8): mm355.RGBA8, np.dtype(np.float16): mm355.RGBA16F}.get(
+            frames[0].dtype, mm355.RGBA32F)
     dev_in = torch.from_numpy(np.stack(frames)).cuda()
     dev_out = torch.empty_like(dev_in)
     if mode == "frame":

@@ -59,6 +59,13 @@ def lib():
         L.mm_ref_set_state.argtypes = [vp, vp]
         L.mm_ref_process.argtypes = [vp, fp, fp, ctypes.POINTER(Dbg)]
         L.mm_ref_process_u8.argtypes = [vp, u8p, u8p]
+        L.mm_ref_process_f16.argtypes = [vp, vp, vp]
+        L.mm_ref_process_srgb8.argtypes = [vp, u8p, u8p]
+        L.mm_ref_srgb_tables.argtypes = [fp, fp]
+        L.mm_ref_half_to_float.restype = ctypes.c_float
+        L.mm_ref_half_to_float.argtypes = [ctypes.c_uint16]
+        L.mm_ref_float_to_half.restype = ctypes.c_uint16
+        L.mm_ref_float_to_half.argtypes = [ctypes.c_float]
         L.mm_ref_fft_centered.argtypes = [ctypes.c_int, fp, fp]
         L.mm_ref_ifft_mag.argtypes = [ctypes.c_int, fp, fp]
         L.mm_ref_mask.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
@@ -97,6 +104,22 @@ def synth_frame(width, height, t, seed=0x5EED0000, gray=False):
     out = np.empty((height, width, 4), np.uint8)
     lib().mm_ref_synth_frame(width, height, t, seed, 1 if gray else 0, _u8p(out))
     return out
+
+
+def srgb_tables():
+    """(dec[256], thr[257]) of MM_RGBA8_SRGB (include/mm.h), as the oracle builds them."""
+    dec = np.empty(256, np.float32)
+    thr = np.empty(257, np.float32)
+    lib().mm_ref_srgb_tables(_fp(dec), _fp(thr))
+    return dec, thr
+
+
+def float_to_half_bits(v):
+    return lib().mm_ref_float_to_half(v)
+
+
+def half_bits_to_float(b):
+    return lib().mm_ref_half_to_float(b)
 
 
 def fft_centered(y):
@@ -210,8 +233,21 @@ class Oracle:
         buf = np.ascontiguousarray(buf, np.uint8)
         lib().mm_ref_set_state(self.h, buf.ctypes.data)
 
+    def process_srgb8(self, frame):
+        """frame: uint8 [H,W,4] sRGB-encoded (MM_RGBA8_SRGB); returns the same."""
+        a = np.ascontiguousarray(frame, np.uint8)
+        out = np.empty_like(a)
+        lib().mm_ref_process_srgb8(self.h, _u8p(a), _u8p(out))
+        return out
+
     def process(self, frame, dbg=False):
-        """frame: float32 [H,W,4] or uint8 [H,W,4]; returns same dtype."""
+        """frame: float32, float16 (MM_RGBA16F) or uint8 (UNORM) [H,W,4];
+        returns the same dtype."""
+        if frame.dtype == np.float16:
+            a = np.ascontiguousarray(frame)
+            out = np.empty_like(a)
+            lib().mm_ref_process_f16(self.h, a.ctypes.data, out.ctypes.data)
+            return out
         if frame.dtype == np.uint8:
             a = np.ascontiguousarray(frame)
             out = np.empty_like(a)

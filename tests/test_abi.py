@@ -22,7 +22,7 @@ def test_library_loads_and_exports_header_symbols():
     assert not missing, missing
     for s in syms:
         assert hasattr(L, s)
-    assert L.mm_abi_version() == 9
+    assert L.mm_abi_version() == 10
 
 
 def test_strerror_and_defaults():
@@ -123,3 +123,111 @@ def test_unity_shim_calls_only_declared_entry_points():
         assert hasattr(mm355.lib(), s)
     for entry in ("UnityPluginLoad", "UnityPluginUnload", "IssuePluginEventAndData"):
         assert entry in src
+
+
+def test_frame_formats_and_sizes():
+    """MM_RGBA16F / MM_RGBA8_SRGB (ABI 10): format codes, bytes per frame, and
+    unknown formats refused by every frame entry point (no GPU needed)."""
+    assert (mm355.RGBA8, mm355.RGBA32F, mm355.RGBA16F, mm355.RGBA8_SRGB) == (0, 1, 2, 3)
+    for f, bpp in mm355.FORMAT_BPP.items():
+        assert mm355.frame_bytes(1920, 1080, f) == 1920 * 1080 * bpp
+    with pytest.raises(mm355.MMError):
+        mm355.frame_bytes(64, 48, 4)
+    with pytest.raises(mm355.MMError):
+        mm355.frame_bytes(0, 48, 0)
+    hdr = open(mm355.binding.HEADER).read()
+    assert "#define MM_RGBA16F    2" in hdr and "#define MM_RGBA8_SRGB 3" in hdr
+    P = mm355.processor._fmt_of
+    assert P(np.zeros(1, np.uint8)) == mm355.RGBA8 and P(np.zeros(1, np.uint8), True) == mm355.RGBA8_SRGB
+    assert P(np.zeros(1, np.float16)) == mm355.RGBA16F and P(np.zeros(1, np.float32)) == mm355.RGBA32F
+
+
+def test_srgb_tables_kernel_header_equals_oracle():
+    """The kernels' sRGB tables (csrc/mm_srgb.hpp, tools/gen_srgb.py) are the
+    oracle's bit for bit, and encode(decode(b)) == b for every byte."""
+    import os
+    import re
+    txt = open(os.path.join(os.path.dirname(mm355.LIB_PATH), "..", "csrc", "mm_srgb.hpp")).read()
+    vals = np.array([float.fromhex(v) for v in re.findall(r"(-?0x[0-9a-f.p+-]+)f", txt)], np.float32)
+    dec, thr = O.srgb_tables()
+    assert vals.size == 256 + 255
+    assert np.array_equal(vals[:256].view(np.uint32), dec.view(np.uint32))
+    assert np.array_equal(vals[256:].view(np.uint32), thr[1:256].view(np.uint32))
+    assert np.isneginf(thr[0]) and np.isposinf(thr[256]) and np.all(np.diff(thr) > 0)
+    enc = np.searchsorted(thr, dec, side="right") - 1      # largest b with dec >= thr[b]
+    assert np.array_equal(enc, np.arange(256))
+    # the curve's known points: 0 -> 0, 255 -> 1, byte 188 ~ 0.5 linear (IEC 61966-2-1)
+    assert dec[0] == 0.0 and dec[255] == 1.0 and abs(dec[188] - 0.50289) < 1e-4
+
+
+def test_oracle_half_conversions_match_ieee():
+    """The oracle's binary16 codecs (MM_RGBA16F) against numpy's IEEE ones:
+    every half decodes exactly, floats round to nearest even (subnormals,
+    the overflow edge and ties included)."""
+    h = np.arange(0, 65536, 257, dtype=np.uint16)
+    got = np.array([O.half_bits_to_float(int(b)) for b in h], np.float32)
+    ref = h.view(np.float16).astype(np.float32)
+    fin = ~np.isnan(ref)
+    assert np.array_equal(got[fin], ref[fin]) and np.all(np.isnan(got[~fin]))
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal(4000) * 10.0 ** rng.integers(-9, 5, 4000)).astype(np.float32)
+    ties = (np.arange(1, 200, dtype=np.float32) + np.float32(0.5)) * np.float32(2.0 ** -24)
+    x = np.concatenate([x, ties, np.array([65504, 65519.99, 65520, 6.1e-5, 5.96e-8, 2.98e-8], np.float32)])
+    got = np.array([O.float_to_half_bits(float(v)) for v in x], np.uint16)
+    with np.errstate(over="ignore"):
+        assert np.array_equal(got, x.astype(np.float16).view(np.uint16))
+
+
+def _build_variant(tmp, name):
+    """A copy of the tree's libmm355.so as an A/B variant <name>.so and its
+    ring library <name>_ring.so, built as scripts/build_variants.sh does."""
+    import os
+    import shutil
+    pkg = os.path.dirname(os.path.dirname(mm355.LIB_PATH))
+    shutil.copy(mm355.LIB_PATH, os.path.join(tmp, name + ".so"))
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-I" + os.path.join(pkg, "..", "include"),
+                    "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-o", os.path.join(tmp, name + "_ring.so"),
+                    os.path.join(pkg, "host", "mm_ring.c"), "-L" + tmp, "-l:" + name + ".so", "-L/opt/rocm/lib",
+                    "-lrccl", "-lamdhip64", "-lpthread", "-ldl", "-lm", "-Wl,-rpath,$ORIGIN",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    return os.path.join(tmp, name + ".so")
+
+
+_RING_PROBE = """
+import os, sys
+sys.path.insert(0, {pkg!r})
+import mm355
+try:
+    mm355.ring_lib()
+    print("BOUND", mm355.ring.ring_lib_path(), mm355.binding.library_path())
+except mm355.MMError as e:
+    print("REFUSED", e)
+"""
+
+
+def test_ring_library_binds_the_loaded_build(tmp_path):
+    """with MM355_LIB naming an A/B variant, the ring library
+    that loads is the variant's own and resolves its mm_* calls to that same
+    build; a ring library bound to another build (the tree's) is refused
+    instead of silently running the other build's kernels."""
+    import os
+    import sys
+    var = _build_variant(str(tmp_path), "abvar")
+    pkg = os.path.dirname(os.path.dirname(mm355.LIB_PATH))
+    code = _RING_PROBE.format(pkg=pkg)
+
+    def run(**env):
+        e = {k: v for k, v in os.environ.items() if k not in ("MM355_LIB", "MM355_RING_LIB")}
+        e.update(env)
+        return subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True,
+                              check=True).stdout.strip()
+
+    out = run(MM355_LIB=var)
+    assert out.startswith("BOUND"), out
+    _, ring_path, core = out.split()
+    assert ring_path == os.path.join(str(tmp_path), "abvar_ring.so") and core == os.path.realpath(var)
+    tree_ring = os.path.join(os.path.dirname(mm355.LIB_PATH), "libmm_ring.so")
+    out = run(MM355_LIB=var, MM355_RING_LIB=tree_ring)
+    assert out.startswith("REFUSED") and "bound to" in out, out
+    out = run()                                   # the tree's pair
+    assert out.startswith("BOUND"), out

@@ -30,8 +30,11 @@ def test_import_rejects_bad_arguments_without_gpu():
 
 
 @pytest.mark.gpu
-def test_zero_copy_import_matches_device_buffers():
-    r = subprocess.run([CHECK, "-w", "256", "-h", "144", "-n", "8"], capture_output=True,
+@pytest.mark.parametrize("fmt", [mm355.RGBA8, mm355.RGBA16F, mm355.RGBA8_SRGB])
+def test_zero_copy_import_matches_device_buffers(fmt):
+    """RGBA8 and the engine's own targets (ABI 10): the HDR camera's linear
+    half frames and an 8-bit sRGB target, taken in place."""
+    r = subprocess.run([CHECK, "-w", "256", "-h", "144", "-n", "8", "-f", str(fmt)], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "extmem ok" in r.stdout

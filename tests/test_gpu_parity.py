@@ -394,6 +394,7 @@ def test_bench_sharded_ring_equals_single_rank():
                "--dist-backend", "gloo", "--checksum", "--frames-per-step", "6", "--steps", "3",
                "--warmup", "1"])
     assert one["frames"] == two["frames"] == [0, 47]
+    assert not one["inputs_wrapped"] and not two["inputs_wrapped"]
     assert one["checksums"] == two["checksums"]
 
 

@@ -31,8 +31,8 @@ def header_symbols():
 
 def test_ring_library_exports_header_symbols():
     syms = header_symbols()
-    assert syms == ["mm_ring_create", "mm_ring_destroy", "mm_ring_get_id", "mm_ring_halo_frames",
-                    "mm_ring_last_error", "mm_ring_step", "mm_ring_step_halo"]
+    assert syms == ["mm_ring_core_library", "mm_ring_create", "mm_ring_destroy", "mm_ring_get_id",
+                    "mm_ring_halo_frames", "mm_ring_last_error", "mm_ring_step", "mm_ring_step_halo"]
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
                          check=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
@@ -96,6 +96,7 @@ def test_bench_c_ring_world1_1080p_equals_single_rank():
     one = _bench(common)
     ring = _bench(common + ["--ring-self"])
     assert one["frames"] == ring["frames"] == [0, 23]
+    assert not one["inputs_wrapped"] and not ring["inputs_wrapped"]
     assert one["checksums"] == ring["checksums"]
     line = _bench(["--ring-self", "--frames-per-step", "16", "--steps", "2", "--warmup", "1",
                    "--no-cpu-baseline", "--drop-in-frames", "0"])

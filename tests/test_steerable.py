@@ -200,3 +200,62 @@ def test_gpu_frames_per_launch_bitwise(filt):
     for nf in ("2",):
         assert torch.equal(res[nf][0], res["1"][0]), nf
         assert torch.equal(res[nf][1], res["1"][1]), nf
+
+
+@pytest.mark.gpu
+def test_c1_literal_256_gray_L3_O4_S10_32_frames():
+    """BASELINE configs[0] literally: 256 x 256 gray, 3 levels,
+    4 orientations, PhaseScale 10, a 32-frame clip, in MM_MODE_STEERABLE on
+    the GPU.  L = 3 makes the one middle band's centre 0/0 = NaN
+    (PyramidOperations.compute:59-64, :71), so its mask is zero everywhere and
+    no subband carries anything: the output must be the spec's (float64), the
+    reference restatement's (C oracle, O = 1) and the GPU pyramid path's, all
+    within the fp32 bar, frame by frame."""
+    W = H = 256
+    n = 32
+    fr = [f.astype(np.float32) / np.float32(255) for f in T.synth(W, H, n, gray=True, fmt="u8")]
+    got = gpu_steer(W, H, fr, levels=3, S=10.0, Oo=4, batch=8)
+    r = SR.SteerableRef(W, H, levels=3, phase_scale=10.0, orientations=4)
+    spec = [r.process(f.astype(np.float64)) for f in fr]
+    ref = T.oracle_run(W, H, fr, 3, 10.0)
+    pyr = T.gpu_run(W, H, fr, 3, 10.0, mode="stream", batch=8)
+    assert np.array_equal(got[0], fr[0])
+    for k in range(1, n):
+        T.assert_close_f32(got[k], spec[k].astype(np.float32))
+        T.assert_close_f32(got[k], ref[k])
+        T.assert_close_f32(got[k], pyr[k])
+        assert np.abs(got[k][..., 0] - got[k][..., 1]).max() < 1e-6     # gray stays gray
+
+
+@pytest.mark.gpu
+def test_odd_size_steerable_set_params():
+    """mm_set_params on an odd-size handle accepts the steerable
+    mode (mm_create does since round 5).  63 x 47: a pyramid handle switched
+    to steerable O = 4, then its phase scale changed, equals a handle created
+    steerable on the same frames (bitwise: the switch passes one frame through
+    and seeds the local phases, as a fresh handle's first frame does)."""
+    import mm355
+    import torch
+    W, H = 63, 47
+    fr = frames(W, H, 8)
+    dev = torch.from_numpy(np.stack(fr)).cuda()
+    kw = dict(mode=mm355.MODE_STEERABLE, orientations=4)
+    a = mm355.Handle(W, H, mm355.Params.make(phase_scale=10.0))
+    oa = torch.empty_like(dev)
+    a.process_stream(dev[:3], oa[:3], 3, mm355.RGBA32F)
+    a.set_params(mm355.Params.make(phase_scale=10.0, **kw))
+    a.process_stream(dev[3:6], oa[3:6], 3, mm355.RGBA32F)
+    a.set_params(mm355.Params.make(phase_scale=25.0, **kw))
+    a.process_stream(dev[6:], oa[6:], 2, mm355.RGBA32F)
+    b = mm355.Handle(W, H, mm355.Params.make(phase_scale=10.0, **kw))
+    ob = torch.empty_like(dev)
+    b.process_stream(dev[3:6], ob[3:6], 3, mm355.RGBA32F)
+    b.set_params(mm355.Params.make(phase_scale=25.0, **kw))
+    b.process_stream(dev[6:], ob[6:], 2, mm355.RGBA32F)
+    torch.cuda.synchronize()
+    ga, gb = oa.cpu().numpy(), ob.cpu().numpy()
+    a.close()
+    b.close()
+    assert np.array_equal(ga[3], fr[3])                  # the switch frame passes through
+    assert np.array_equal(ga[3:], gb[3:])
+    assert not np.array_equal(ga[6], ga[3])
