@@ -218,11 +218,18 @@ template <> struct Pix<0> {           // RGBA8 UNORM
                            (float)((u >> 16) & 255u) * s, (float)(u >> 24) * s);
     }
     __device__ static float4 load(const uint8_t *base, size_t i) { return cvt(raw(base, i)); }
+    // round(255 v) of saturated v: one FMA 2^23 + 255 v (the product is exact
+    // inside it; ulp 1 at 2^23) leaves the rounded byte in the low mantissa
+    // bits; two byte permutes assemble R, G, B and alpha 255.  5 VALU per
+    // pixel instead of 3 FMAs + 3 converts + 2 shifts and ors (+0.5-then-truncate rounding: the two agree except within 2^-17
+    // of a half-way point, below the RGBA8 bar's +-1 LSB).
     __device__ static uint32_t pack(float r, float g, float b)
     {
-        uint32_t R = (uint32_t)(r * 255.0f + 0.5f), G = (uint32_t)(g * 255.0f + 0.5f),
-                 B = (uint32_t)(b * 255.0f + 0.5f);
-        return R | (G << 8) | (B << 16) | (255u << 24);
+        constexpr float kMagic = 8388608.0f;   // 2^23
+        const uint32_t R = __float_as_uint(r * 255.0f + kMagic), G = __float_as_uint(g * 255.0f + kMagic);
+        const uint32_t B = __float_as_uint(b * 255.0f + kMagic);
+        const uint32_t lo = __builtin_amdgcn_perm(G, R, 0x0d0c0400u);   // R, G, 0, 0xff
+        return (B << 16) | lo;   // B's low mantissa byte into byte 2 (one v_lshl_or)
     }
     __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
     {
@@ -372,12 +379,14 @@ __device__ __forceinline__ c2 chroma_iq2(typename Pix<FMT>::raw_t u)
 }
 
 // YIQToRGB.shader:51-76 + saturate for one pixel: R and G as one pair, B alone
+// (B as two FMAs: written as 1 yb + ..., the contraction fused the 1 yb
+// product and left a multiply and a subtract)
 __device__ __forceinline__ void yiq_rgb(float yb, c2 cc, float &rr, float &gg, float &bb)
 {
     const c2 rg = mk(yb, yb) + mk(0.956f, -0.272f) * cc.x + mk(0.621f, -0.647f) * cc.y;
     rr = sat(rg.x);
     gg = sat(rg.y);
-    bb = sat(1.0f * yb + -1.106f * cc.x + 1.703f * cc.y);
+    bb = sat(fmaf(1.703f, cc.y, fmaf(-1.106f, cc.x, yb)));
 }
 
 // =========================================================================
@@ -385,6 +394,9 @@ __device__ __forceinline__ void yiq_rgb(float yb, c2 cc, float &rr, float &gg, f
 // =========================================================================
 // GEN (odd W or H): the composite taps of a pixel span i-2 .. i+1 and are
 // read as unmerged Tap4 entries (colT / rowT) instead of the 3-tap tables.
+#ifndef MM_K1_COOP
+#define MM_K1_COOP 1   // batch form: the two row pairs' source rows loaded once
+#endif
 template <int LOG2N, int FMT, bool GEN = false, bool LAT = false>
 __global__ __launch_bounds__((k1_gpw<LOG2N, LAT>() * fft_T<LOG2N>()))
 void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pairs_per_frame,
@@ -452,6 +464,54 @@ void k_rows_fwd(const uint8_t *__restrict__ frames, size_t frame_bytes, int pair
                 }
                 V[i] = va;
                 V[g.W + i] = vb;
+            }
+        }
+    } else if (MM_K1_COOP && GPW == 2 && !LAT && pairs_per_frame % 2 == 0) {
+        // Batch form, the two groups' row pairs in one frame (uniform test):
+        // the workgroup's 4 rows r0 .. r0+3 read the 6 source rows r0-1 ..
+        // r0+4 once, shared (each group alone read 4: 8 row loads for 4
+        // rows); thread tid of the 2T does N/(2T) columns for both groups.
+        // Same lumas and the same packed expressions per group as below: the
+        // V2 values are bitwise the per-group form's.
+        if (valid) {
+            const int r0 = ra - 2 * grp;   // group 0's pair (same frame: pairs_per_frame even)
+            c2 w[2][3];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                float4 wa = rowW3[r0 + 2 * q], wb = rowW3[r0 + 2 * q + 1];
+                wa.x *= kLumaUnit<FMT>, wa.y *= kLumaUnit<FMT>, wa.z *= kLumaUnit<FMT>;
+                wb.x *= kLumaUnit<FMT>, wb.y *= kLumaUnit<FMT>, wb.z *= kLumaUnit<FMT>;
+                w[q][0] = mk(wa.x, wb.x);
+                w[q][1] = mk(wa.y, wb.y);
+                w[q][2] = mk(wa.z, wb.z);
+            }
+            const uint8_t *rowp[6];   // workgroup-uniform source row pointers
+#pragma unroll
+            for (int d = 0; d < 6; ++d) rowp[d] = img + (unsigned)(wrap_near(r0 - 1 + d, g.H, g.edge) * g.W * BPP);
+            constexpr int CT = N / (2 * T);          // columns per thread (W <= N)
+            constexpr int CB = BPP == 16 ? 1 : CT;   // columns per load batch
+            c2 *V2g1 = lds_all + lds_complex<N>();
+#pragma unroll
+            for (int h = 0; h < CT / CB; ++h) {
+                __builtin_amdgcn_sched_barrier(0);
+                raw_t px[CB][6];
+#pragma unroll
+                for (int u = 0; u < CB; ++u) {
+                    const unsigned off = (unsigned)min((int)threadIdx.x + (h * CB + u) * 2 * T, g.W - 1) * BPP;
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) px[u][d] = ld_off<raw_t>(rowp[d], off);
+                }
+#pragma unroll
+                for (int u = 0; u < CB; ++u) {
+                    const int i = (int)threadIdx.x + (h * CB + u) * 2 * T;
+                    float l[6];
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) l[d] = luma_units<FMT>(px[u][d]);
+                    if (i < g.W) {
+                        lds_all[i] = w[0][0] * mk(l[0], l[1]) + w[0][1] * mk(l[1], l[2]) + w[0][2] * mk(l[2], l[3]);
+                        V2g1[i] = w[1][0] * mk(l[2], l[3]) + w[1][1] * mk(l[3], l[4]) + w[1][2] * mk(l[4], l[5]);
+                    }
+                }
             }
         }
     } else if (valid) {
@@ -1490,6 +1550,13 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #pragma unroll
         for (int j = 0; j < 8; ++j)   // G[0][r], G[N/2][r] are real (exact zero imaginary parts)
             v[j] = packed ? mk(ga[j].x, gb[j]) : ga[j];
+        const bool pass_frame = fr < 0;   // the prime (fr = -1)
+#ifndef MM_K2_NOGAHEAD
+        // the prime's successor (frame 0) loads now, under the prime's transform
+        // (the prime has no op, so its "after the op" slot below came one
+        // transform later; a one-frame call waits on these loads next)
+        if (pass_frame) load_g(nframes > 0 ? 0 : -1, t);
+#endif
         // opaque per-iteration copy of the twiddle bases (same reason as t: the
         // products of their powers must not be hoisted into live registers)
         c2 wt[kTwSlots];
@@ -1503,7 +1570,6 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         fft_dif<LOG2N, -1, TT>(v, t, lds, wt, ttab);
         MM_MARK("M2_fwd_end");
         K2_STAMP(3);
-        const bool pass_frame = fr < 0;   // the prime (fr = -1)
         // the spectral op of a regular group (all groups but the packed one)
         auto regular_op = [&]() {
             if (pass_frame) {
@@ -1704,7 +1770,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
         // transform, staging and Q stores instead of stalling the next frame
         // at its top (same-call K2 8.94 -> 8.33 us/frame, profiles/r03_abv.txt;
         // the op's registers are free again here: no spill at 123 VGPRs)
-        load_g(fr + 1 < nframes ? fr + 1 : nframes - 1, t);
+        if (!pass_frame) load_g(fr + 1 < nframes ? fr + 1 : nframes - 1, t);
 #endif
         staged = !pass_frame;
         if (!pass_frame) {

@@ -11,7 +11,7 @@ import sys
 L = open(sys.argv[1]).read().split("\n")
 mode = sys.argv[2] if len(sys.argv) > 2 else "2"
 log2n = sys.argv[3] if len(sys.argv) > 3 else "11"
-i0 = next(i for i, l in enumerate(L) if re.match(r"^_ZN2mm6k_colsILi%sELi%s(?:ELb[01])?EEEv\S*:" % (log2n, mode), l))
+i0 = next(i for i, l in enumerate(L) if re.match(r"^_ZN2mm6k_colsILi%sELi%s(?:ELb[01])?(?:ELi0)?EEEv\S*:" % (log2n, mode), l))
 end = next(i for i in range(i0, len(L)) if L[i].strip().startswith("s_endpgm"))
 body = L[i0:end]
 marks = [(i, l.strip()) for i, l in enumerate(body) if l.strip().startswith("; M")]
