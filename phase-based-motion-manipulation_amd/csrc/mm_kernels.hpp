@@ -218,18 +218,11 @@ template <> struct Pix<0> {           // RGBA8 UNORM
                            (float)((u >> 16) & 255u) * s, (float)(u >> 24) * s);
     }
     __device__ static float4 load(const uint8_t *base, size_t i) { return cvt(raw(base, i)); }
-    // round(255 v) of saturated v: one FMA 2^23 + 255 v (the product is exact
-    // inside it; ulp 1 at 2^23) leaves the rounded byte in the low mantissa
-    // bits; two byte permutes assemble R, G, B and alpha 255.  5 VALU per
-    // pixel instead of 3 FMAs + 3 converts + 2 shifts and ors (+0.5-then-truncate rounding: the two agree except within 2^-17
-    // of a half-way point, below the RGBA8 bar's +-1 LSB).
     __device__ static uint32_t pack(float r, float g, float b)
     {
-        constexpr float kMagic = 8388608.0f;   // 2^23
-        const uint32_t R = __float_as_uint(r * 255.0f + kMagic), G = __float_as_uint(g * 255.0f + kMagic);
-        const uint32_t B = __float_as_uint(b * 255.0f + kMagic);
-        const uint32_t lo = __builtin_amdgcn_perm(G, R, 0x0d0c0400u);   // R, G, 0, 0xff
-        return (B << 16) | lo;   // B's low mantissa byte into byte 2 (one v_lshl_or)
+        uint32_t R = (uint32_t)(r * 255.0f + 0.5f), G = (uint32_t)(g * 255.0f + 0.5f),
+                 B = (uint32_t)(b * 255.0f + 0.5f);
+        return R | (G << 8) | (B << 16) | (255u << 24);
     }
     __device__ static void store(uint8_t *base, unsigned i, float r, float g, float b)
     {
@@ -1276,6 +1269,14 @@ __device__ unsigned long long mm_k2_exit[4096 * 8];    // ... after the last Q s
 // the forward transform as a passthrough frame (fr = -1), which sets F_{t-1}
 // in registers bit for bit as the frame loop would have, then frames
 // 0 .. nframes-1 of G, whose Q go to Q + fr * q_stride.
+// A per-bin table entry from LDS as its own ds_read_b64 (lds_ld: not paired
+// into a ds_read2_b64, which costs twice the LDS cycles on gfx950)
+__device__ __forceinline__ float2 tab_ld(const float2 *p)
+{
+    const c2 v = lds_ld(reinterpret_cast<const c2 *>(p));
+    return make_float2(v.x, v.y);
+}
+
 template <int LOG2N, int MODE, bool BLK0, int SP = 0>
 __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const c2 *Gprev, c2 *Q,
                                             size_t q_stride, int nframes, const Geo &g,
@@ -1596,8 +1597,8 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
 #endif
                 for (int j = 0; j < 8; j += 2) {   // two bins per packed op
                     if (j % MM_K2_OPX2G == 0) __builtin_amdgcn_sched_barrier(0);
-                    const float2 mt0 = j < 4 ? tlo[j * (N / 8) / C] : thi[(N - j * (N / 8)) / C];
-                    const float2 mt1 = j + 1 < 4 ? tlo[(j + 1) * (N / 8) / C] : thi[(N - (j + 1) * (N / 8)) / C];
+                    const float2 mt0 = tab_ld(j < 4 ? tlo + j * (N / 8) / C : thi + (N - j * (N / 8)) / C);
+                    const float2 mt1 = tab_ld(j + 1 < 4 ? tlo + (j + 1) * (N / 8) / C : thi + (N - (j + 1) * (N / 8)) / C);
                     if constexpr (SP > 0)
                         pyramid_op_pow_x2<SP, false>(v[j], prev[j], mt0, 0.0f, v[j + 1], prev[j + 1], mt1, 0.0f, sp);
                     else
@@ -1628,7 +1629,7 @@ __device__ __forceinline__ void k_cols_body(const c2 *G, size_t g_stride, const 
                     if (j % MM_K2_OPX2G == 0) __builtin_amdgcn_sched_barrier(0);
                     const int i0 = j < 4 ? j * (N / 8) / C : (N - j * (N / 8)) / C;
                     const int i1 = j + 1 < 4 ? (j + 1) * (N / 8) / C : (N - (j + 1) * (N / 8)) / C;
-                    const float2 mt0 = j < 4 ? tlo[i0] : thi[i0], mt1 = j + 1 < 4 ? tlo[i1] : thi[i1];
+                    const float2 mt0 = tab_ld(j < 4 ? tlo + i0 : thi + i0), mt1 = tab_ld(j + 1 < 4 ? tlo + i1 : thi + i1);
                     const float s0 = j < 4 ? mlo[i0] : mhi[i0], s1 = j + 1 < 4 ? mlo[i1] : mhi[i1];
                     if constexpr (SP > 0)
                         pyramid_op_pow_x2<SP, true>(v[j], prev[j], mt0, s0, v[j + 1], prev[j + 1], mt1, s1, sp);

@@ -8,7 +8,7 @@
  *
  *   mm_cli [-w W] [-h H] [-n frames] [-l levels] [-s phase_scale]
  *          [-b frames_per_call] [-i in.{rgba,y4m}] [-o out.{rgba,y4m}] [-d device]
- *          [--full-range] [--standard] [--show-magnitude] [--show-phase]
+ *          [--full-range] [--srgb] [--standard] [--show-magnitude] [--show-phase]
  *          [--orientations O] [--iir] [--halo K]
  *          [--checksum] [--ring-world G --ring-rank R --ring-id FILE]
  *          [--ring-local G [--compare]]
@@ -36,6 +36,9 @@
  * .y4m input: 8-bit 4:2:0 / 4:4:4 / mono YUV4MPEG2, geometry from its header
  * (host/y4m.h, BT.601 limited range unless --full-range); .y4m output is 4:4:4
  * at the input's frame rate.  Any other extension is raw RGBA8 (-w/-h).
+ * --srgb: the 8-bit frames are sRGB-encoded (video and display-referred
+ * clips are), processed in linear light as Unity's Linear colour space does
+ * (MM_RGBA8_SRGB: decoded on read, encoded on write); default UNORM.
  */
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
@@ -52,6 +55,9 @@
 
 #include <time.h>
 #include <unistd.h>
+
+/* frame format of every 8-bit frame this driver moves (--srgb) */
+static int g_fmt = MM_RGBA8;
 
 #define CHECK(x)                                                                      \
     do {                                                                              \
@@ -143,7 +149,7 @@ static int run_ring(mm_handle *h, int W, int H, int F, int B, int dev, int world
         return 1;
     }
     mm_ring *r = NULL;
-    int rc = mm_ring_create(world, rank, id, dev, h, W, H, B, MM_RGBA8, &r);
+    int rc = mm_ring_create(world, rank, id, dev, h, W, H, B, g_fmt, &r);
     if (rc) {
         fprintf(stderr, "mm_ring_create: %s (%s)\n", mm_strerror(rc), mm_ring_last_error());
         return 1;
@@ -219,7 +225,7 @@ static void *local_rank_main(void *arg)
     a->rc = 1;
     if (hipSetDevice(a->dev) != hipSuccess) { snprintf(a->err, sizeof a->err, "hipSetDevice"); return NULL; }
     if ((rc = mm_create(a->W, a->H, a->p, a->dev, &h)) || (rc = mm_set_batch(h, a->B)) ||
-        (rc = mm_ring_create_local(a->hub, a->rank, a->dev, h, a->W, a->H, a->B, MM_RGBA8, &r))) {
+        (rc = mm_ring_create_local(a->hub, a->rank, a->dev, h, a->W, a->H, a->B, g_fmt, &r))) {
         snprintf(a->err, sizeof a->err, "setup: %s (%s)", mm_strerror(rc), mm_ring_last_error());
         /* a rank that cannot join would leave the others at the hub's
          * barrier: report and stop the process */
@@ -294,7 +300,7 @@ static int compare_single(const mm_params *p, int W, int H, int F, int B, int de
     int max_all = 0;
     for (int f0 = 0; f0 < F; f0 += B) {
         CHECK(mm_synth_frames(d_in, W, H, f0, B, 0x5EED0000ull, 0, s));
-        CHECK(mm_process_stream(h, d_in, d_out, B, MM_RGBA8, s));
+        CHECK(mm_process_stream(h, d_in, d_out, B, g_fmt, s));
         if (hipStreamSynchronize(s) != hipSuccess) return 1;
         for (int k = 0; k < B; ++k) {
             if (hipMemcpy(a, (unsigned char *)d_out + fb * k, fb, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -384,6 +390,7 @@ int main(int argc, char **argv)
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         if (!strcmp(a, "--full-range")) { full_range = 1; continue; }
+        if (!strcmp(a, "--srgb")) { g_fmt = MM_RGBA8_SRGB; continue; }
         if (!strcmp(a, "--standard")) { standard = 1; continue; }
         if (!strcmp(a, "--show-magnitude")) { show_mag = 1; continue; }
         if (!strcmp(a, "--show-phase")) { show_phase = 1; continue; }
@@ -508,7 +515,7 @@ int main(int argc, char **argv)
             CHECK(mm_synth_frames(d_in, W, H, done, n, 0x5EED0000ull, 0, s));
         }
         hipEventRecord(e0, s);
-        CHECK(mm_process_stream(h, d_in, d_out, n, MM_RGBA8, s));
+        CHECK(mm_process_stream(h, d_in, d_out, n, g_fmt, s));
         hipEventRecord(e1, s);
         hipEventSynchronize(e1);
         float ms = 0.0f;

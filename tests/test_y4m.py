@@ -120,8 +120,10 @@ def test_rejects_unsupported(y4m, tmp_path, hdr):
 
 
 @pytest.mark.gpu
-def test_cli_y4m_matches_binding(y4m, tmp_path):
-    """mm_cli on a Y4M clip == the same decoded frames through the binding."""
+@pytest.mark.parametrize("srgb", [False, True])
+def test_cli_y4m_matches_binding(y4m, tmp_path, srgb):
+    """mm_cli on a Y4M clip == the same decoded frames through the binding
+    (--srgb: the clip's 8-bit RGB taken as sRGB-encoded, MM_RGBA8_SRGB)."""
     import mm355
     import torch
     W, H, n = 64, 48, 5
@@ -135,14 +137,14 @@ def test_cli_y4m_matches_binding(y4m, tmp_path):
     src, dst = str(tmp_path / "in.y4m"), str(tmp_path / "out.y4m")
     write_y4m(src, clip, W, H)
     subprocess.check_call([CLI, "-i", src, "-o", dst, "-n", str(n), "-l", "5", "-s", "10",
-                           "-b", "2"], timeout=120)
+                           "-b", "2"] + (["--srgb"] if srgb else []), timeout=120)
     _, frames = read_all(y4m, src)
     _, got = read_all(y4m, dst)
     assert len(got) == n
     h = mm355.Handle(W, H, mm355.Params.make(levels=5, phase_scale=10.0))
     dev = torch.from_numpy(np.stack(frames)).cuda()
     out = torch.empty_like(dev)
-    h.process_stream(dev, out, n, mm355.RGBA8)
+    h.process_stream(dev, out, n, mm355.RGBA8_SRGB if srgb else mm355.RGBA8)
     torch.cuda.synchronize()
     h.close()
     L, _ = y4m
