@@ -436,6 +436,9 @@ static int set_attrs(int W)
         for (int f = 0; f < 4; ++f)
             MM_FMT_SWITCH(f, HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose<12, FMT_>),
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds)))
+        // k_sb_cols: exchange buffers (73.7 KB) + its own staging (run_steer)
+        HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_cols<12>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
     if constexpr (LOG2N == 13) {   // N = 8192: one 8192-point transform per workgroup, 73.7 KB and more
         auto set = [](const void *f, size_t b) {
@@ -810,10 +813,16 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         for (int f = 0; f < nf; ++f) {
             ProfScope ps(h, s, MM_K_COLS, 0);
             const int g2 = sb_groups<LOG2N>();
-            // the staging [Hn][GPW] gets its own LDS area where two workgroups
-            // per CU still fit (1080p: 54 KB), else it aliases the exchange buffers
+            // the staging [Hn][GPW] gets its own LDS area where it costs no
+            // residency: two workgroups per CU at N <= 2048 (1080p: 54 KB
+            // each), and at N = 4096, whose 1,024-thread workgroups are alone
+            // on their CU anyway (126 VGPRs: 4 waves per SIMD), within the
+            // CU's 160 KB (2160p: 73.7 + 34.6 KB); else it aliases the
+            // exchange buffers (one more barrier per band, and a band's
+            // stores cannot overlap the next band's transform)
             const size_t lx = sizeof(c2) * (size_t)g2 * lds_complex<N>(), ls = sizeof(c2) * (size_t)g2 * h->geo.Hn;
-            const int own = h->sb_stg_own && lx + ls <= 81920 ? 1 : 0;
+            const size_t own_cap = sb_threads<LOG2N>() >= 1024 ? 160 * 1024 : 81920;
+            const int own = h->sb_stg_own && lx + ls <= own_cap ? 1 : 0;
             hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),
                                lx + (own ? ls : 0), s, h->d_Fb + fstride * (k + f),
                                h->d_T + t_stride * f, band_stride, h->geo, h->spec, h->d_tw, own);
