@@ -228,6 +228,14 @@ template <> struct Pix<0> {           // RGBA8 UNORM
     {
         st_stream<uint32_t>(base, i * 4u, pack(r, g, b));
     }
+    // r, g, b in code units (255 x the UNORM value), unclamped: three
+    // v_cvt_pk_u8_f32, each rounding to nearest and clamping to 0 .. 255 into
+    // its byte lane (the compose kernels' pack, kOut255)
+    __device__ static uint32_t pack255(float r, float g, float b)
+    {
+        const uint32_t a = __builtin_amdgcn_cvt_pk_u8_f32(r, 0u, 0xff000000u);
+        return __builtin_amdgcn_cvt_pk_u8_f32(b, 2u, __builtin_amdgcn_cvt_pk_u8_f32(g, 1u, a));
+    }
 };
 template <> struct Pix<1> {           // RGBA32F
     static constexpr int bpp = 16;
@@ -313,6 +321,30 @@ template <> struct Pix<3> {
 };
 // saturated before the store: the UNORM destinations (RGBA8, RGBA8 sRGB)
 template <int FMT> constexpr bool kUnorm = FMT == 0 || FMT == 3;
+// MM_OUT255=1 (diagnostic): RGBA8 compose in code units.  The chroma
+// conversion drops its 1/255, the vertical luma blur carries 255 in its
+// weights, and YIQToRGB's saturate and the x255 + round of the UNORM write
+// become the clamp and round-to-nearest-even of v_cvt_pk_u8_f32
+// (Pix<0>::pack255; tools/cvtpk_probe.hip): 3 VALU per pixel instead of 10,
+// K34 -10 % VALU, parity green, but 4 spills at its 128-VGPR bound at
+// N = 2048: same-call K34 6.09 -> 6.24 us per frame at 1080p, equal at 2160p
+// (profiles/r06f_out255_ab.txt).  Off by default.
+#ifndef MM_OUT255
+#define MM_OUT255 0
+#endif
+template <int FMT> constexpr bool kOut255 = MM_OUT255 && FMT == 0;
+// the vertical blur weights of the compose (255 x for kOut255; scalar
+// registers like the kernel argument they come from, not 3 VGPRs)
+__device__ __forceinline__ float uniform_f(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+template <int FMT> __device__ __forceinline__ Blur5 vblur_w(Blur5 b)
+{
+    if constexpr (kOut255<FMT>)
+        return Blur5{uniform_f(b.w0 * 255.0f), uniform_f(b.w1 * 255.0f), uniform_f(b.w2 * 255.0f)};
+    else return b;
+}
 
 // RGBToYIQ.shader:46-50 rows
 __device__ __forceinline__ float luma(float4 c) { return 0.299f * c.x + 0.587f * c.y + 0.114f * c.z; }
@@ -362,7 +394,7 @@ template <int FMT>
 __device__ __forceinline__ c2 chroma_iq2(typename Pix<FMT>::raw_t u)
 {
     if constexpr (FMT == 0) {
-        constexpr float k = 1.0f / 255.0f;
+        constexpr float k = kOut255<FMT> ? 1.0f : 1.0f / 255.0f;
         const float r = (float)(u & 255u), gg = (float)((u >> 8) & 255u), b = (float)((u >> 16) & 255u);
         return mk(0.596f * k, 0.211f * k) * r + mk(-0.274f * k, -0.523f * k) * gg + mk(-0.322f * k, 0.312f * k) * b;
     } else {
@@ -374,12 +406,28 @@ __device__ __forceinline__ c2 chroma_iq2(typename Pix<FMT>::raw_t u)
 // YIQToRGB.shader:51-76 + saturate for one pixel: R and G as one pair, B alone
 // (B as two FMAs: written as 1 yb + ..., the contraction fused the 1 yb
 // product and left a multiply and a subtract)
+// (kOut255: yb, cc and the result in code units, the saturate left to the pack)
+template <int FMT>
 __device__ __forceinline__ void yiq_rgb(float yb, c2 cc, float &rr, float &gg, float &bb)
 {
     const c2 rg = mk(yb, yb) + mk(0.956f, -0.272f) * cc.x + mk(0.621f, -0.647f) * cc.y;
-    rr = sat(rg.x);
-    gg = sat(rg.y);
-    bb = sat(fmaf(1.703f, cc.y, fmaf(-1.106f, cc.x, yb)));
+    const float b = fmaf(1.703f, cc.y, fmaf(-1.106f, cc.x, yb));
+    if constexpr (kOut255<FMT>) {
+        rr = rg.x; gg = rg.y; bb = b;
+    } else {
+        rr = sat(rg.x); gg = sat(rg.y); bb = sat(b);
+    }
+}
+// the compose kernels' packed pixel and single-pixel store of yiq_rgb's result
+template <int FMT> __device__ __forceinline__ uint32_t out_pack(float r, float g, float b)
+{
+    if constexpr (kOut255<FMT>) return Pix<FMT>::pack255(r, g, b);
+    else return Pix<FMT>::pack(r, g, b);
+}
+template <int FMT> __device__ __forceinline__ void out_store(uint8_t *base, unsigned i, float r, float g, float b)
+{
+    if constexpr (kOut255<FMT>) st_stream<uint32_t>(base, i * 4u, Pix<FMT>::pack255(r, g, b));
+    else Pix<FMT>::store(base, i, r, g, b);
 }
 
 // =========================================================================
@@ -2124,17 +2172,18 @@ void k_compose(const float *__restrict__ Yh, size_t yh_stride, const uint8_t *__
         hc[sr] = wc.x * a + wc.y * m + wc.z * c;
     }
     uint8_t *outp = frames_out + (size_t)frame * frame_bytes;
+    const Blur5 bv = vblur_w<FMT>(bw);
 #pragma unroll
     for (int r = 0; r < TR; ++r) {
         const int i = i0 + r;
         if (i < g.H) {
             const float4 wr = rowW3[i];                        // source rows i-1, i, i+1
             const c2 cc = wr.x * hc[r] + wr.y * hc[r + 1] + wr.z * hc[r + 2];   // (ci, cq)
-            const float yb = bw.w0 * yv[r + 2] + bw.w1 * (yv[r + 1] + yv[r + 3]) +
-                             bw.w2 * (yv[r] + yv[r + 4]);
+            const float yb = bv.w0 * yv[r + 2] + bv.w1 * (yv[r + 1] + yv[r + 3]) +
+                             bv.w2 * (yv[r] + yv[r + 4]);
             float rr, gg, bb;
-            yiq_rgb(yb, cc, rr, gg, bb);
-            Pix<FMT>::store(outp + (unsigned)(i * g.W * Pix<FMT>::bpp), (unsigned)X, rr, gg, bb);
+            yiq_rgb<FMT>(yb, cc, rr, gg, bb);
+            out_store<FMT>(outp + (unsigned)(i * g.W * Pix<FMT>::bpp), (unsigned)X, rr, gg, bb);
         }
     }
 }
@@ -2197,6 +2246,7 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
     const unsigned cr = (unsigned)wrap_near(X + 4, g.W, g.edge);
     // horizontally combined I/Q of one source row for the quad (k_compose's
     // staged 3-tap combine over columns X-1 .. X+4)
+    const Blur5 bv = vblur_w<FMT>(bw);   // the compose's vertical blur
     auto chroma_row = [&](int i, c2 (&hc)[4]) {
         const int row = wrap_near(min(i, g.H), g.H, g.edge);
         const unsigned base = (unsigned)(row * g.W);
@@ -2240,11 +2290,14 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
         const int ka_ = i0 + 4 * s_ + 2 * grp;
         const int kl = ka_ < g.Hn ? ka_ : 0;
         const float4 *Qp = reinterpret_cast<const float4 *>(Qf + (size_t)(kl / TK) * g.Qs * TK + (kl % TK));
+        // column ff = t + jT (j < 4) or N - t - jT (j >= 4; = N/2 at t = 0,
+        // j = 4): a workgroup-uniform base per j plus one of two per-thread
+        // offsets, not eight loop-invariant VGPR offsets
+        const unsigned up = (unsigned)t * (TK / 2), dn = (unsigned)(T - 1 - t) * (TK / 2);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int fq = t + j * T;
-            const int ff = fq > N / 2 ? N - fq : fq;
-            qv[j] = Qp[(size_t)ff * (TK / 2)];
+            if (j < 4) qv[j] = (Qp + (size_t)(j * T) * (TK / 2))[up];
+            else qv[j] = (Qp + (size_t)(N - j * T - (T - 1)) * (TK / 2))[dn];
         }
     };
 #ifndef MM_K34_QPF
@@ -2330,21 +2383,23 @@ void k_rows_inv_compose(const c2 *__restrict__ Q, size_t q_stride,
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const c2 cc = wr.x * hc[r][k] + wr.y * hc[r + 1][k] + wr.z * hc[r + 2][k];
-                        const float yb = bw.w0 * yw[r + 2][k] + bw.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
-                                         bw.w2 * (yw[r][k] + yw[r + 4][k]);
-                        yiq_rgb(yb, cc, rr[k], gg[k], bb[k]);
+                        const float yb = bv.w0 * yw[r + 2][k] + bv.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
+                                         bv.w2 * (yw[r][k] + yw[r + 4][k]);
+                        yiq_rgb<FMT>(yb, cc, rr[k], gg[k], bb[k]);
                     }
                     const unsigned o = (unsigned)(i * g.W + X);
                     if constexpr (bpp == 4) {
                         uint4 px;
-                        px.x = Pix<FMT>::pack(rr[0], gg[0], bb[0]);
-                        px.y = Pix<FMT>::pack(rr[1], gg[1], bb[1]);
-                        px.z = Pix<FMT>::pack(rr[2], gg[2], bb[2]);
-                        px.w = Pix<FMT>::pack(rr[3], gg[3], bb[3]);
-                        st_stream<uint4>(outp, o * 4u, px);
+                        px.x = out_pack<FMT>(rr[0], gg[0], bb[0]);
+                        px.y = out_pack<FMT>(rr[1], gg[1], bb[1]);
+                        px.z = out_pack<FMT>(rr[2], gg[2], bb[2]);
+                        px.w = out_pack<FMT>(rr[3], gg[3], bb[3]);
+                        // scalar row base + the thread's column offset: one
+                        // live VGPR, not a hoisted offset per row
+                        st_stream<uint4>(outp + (size_t)(unsigned)(i * g.W) * 4u, (unsigned)X * 4u, px);
                     } else {
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) Pix<FMT>::store(outp, o + k, rr[k], gg[k], bb[k]);
+                        for (int k = 0; k < 4; ++k) out_store<FMT>(outp, o + k, rr[k], gg[k], bb[k]);
                     }
                 }
             }
@@ -2445,6 +2500,7 @@ void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
     const int X = vq ? 4 * q : g.W - 4;
     const unsigned cl = (unsigned)wrap_near(X - 1, g.W, g.edge);
     const unsigned cr = (unsigned)wrap_near(X + 4, g.W, g.edge);
+    const Blur5 bv = vblur_w<FMT>(bw);   // the compose's vertical blur
     auto chroma_row = [&](int i, c2 (&hc)[4]) {   // k_rows_inv_compose's
         const int row = wrap_near(min(i, g.H), g.H, g.edge);
         const unsigned base = (unsigned)(row * g.W);
@@ -2492,21 +2548,21 @@ void k_rows_inv_compose4(const c2 *__restrict__ Q, size_t q_stride,
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const c2 cc = wr.x * hc[r][k] + wr.y * hc[r + 1][k] + wr.z * hc[r + 2][k];
-                const float yb = bw.w0 * yw[r + 2][k] + bw.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
-                                 bw.w2 * (yw[r][k] + yw[r + 4][k]);
-                yiq_rgb(yb, cc, rr[k], gg[k], bb[k]);
+                const float yb = bv.w0 * yw[r + 2][k] + bv.w1 * (yw[r + 1][k] + yw[r + 3][k]) +
+                                 bv.w2 * (yw[r][k] + yw[r + 4][k]);
+                yiq_rgb<FMT>(yb, cc, rr[k], gg[k], bb[k]);
             }
             const unsigned o = (unsigned)(i * g.W + X);
             if constexpr (bpp == 4) {
                 uint4 px;
-                px.x = Pix<FMT>::pack(rr[0], gg[0], bb[0]);
-                px.y = Pix<FMT>::pack(rr[1], gg[1], bb[1]);
-                px.z = Pix<FMT>::pack(rr[2], gg[2], bb[2]);
-                px.w = Pix<FMT>::pack(rr[3], gg[3], bb[3]);
+                px.x = out_pack<FMT>(rr[0], gg[0], bb[0]);
+                px.y = out_pack<FMT>(rr[1], gg[1], bb[1]);
+                px.z = out_pack<FMT>(rr[2], gg[2], bb[2]);
+                px.w = out_pack<FMT>(rr[3], gg[3], bb[3]);
                 st_stream<uint4>(outp, o * 4u, px);
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) Pix<FMT>::store(outp, o + k, rr[k], gg[k], bb[k]);
+                for (int k = 0; k < 4; ++k) out_store<FMT>(outp, o + k, rr[k], gg[k], bb[k]);
             }
         }
     }
