@@ -60,7 +60,7 @@ struct mm_handle {
     float *d_dbg;               // debug view textures [dbg_frames][mag, phase][N][N] (lazily)
     // MM_MODE_STEERABLE (lazily, for the current levels/orientations):
     c2 *d_Fb;                   // per batch frame half spectrum [fb_frames][N/2+1][N] (lazily)
-    c2 *d_T;                    // band rows [nb+1][Hq][N] (row-major, k_sb_cols -> k_sb_rows)
+    c2 *d_T;                    // band rows [nb+1][t_rows(Hn)][N] (row groups, MM_SB_RROWS; k_sb_cols -> k_sb_rows)
     float *d_sst;               // temporal-filter state: phi, u_h, u_l planes [nb][Hn][W+4]
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
@@ -765,7 +765,7 @@ static int steer_alloc(mm_handle *h, hipStream_t s)
     h->steer_nb = -1;
     h->steer_valid = false;
     // band rows of two frames (k_sb_rows runs frames in pairs)
-    if (h_alloc(h, &h->d_T, sizeof(c2) * 2 * (size_t)(nb + 1) * h->N * h->geo.Hq) != hipSuccess ||
+    if (h_alloc(h, &h->d_T, sizeof(c2) * 2 * (size_t)(nb + 1) * h->N * t_rows(h->geo.Hn)) != hipSuccess ||
         h_alloc(h, &h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
@@ -799,7 +799,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
                            fstride, total, h->geo, h->d_tw);
         HIPCHK(hipGetLastError());
     }
-    const size_t band_stride = (size_t)N * h->geo.Hq;
+    const size_t band_stride = (size_t)N * t_rows(h->geo.Hn);
     // DIFF reads and writes only the phi plane (a caller's DIFF state buffer
     // holds just that plane); IIR the three
     const size_t plane = steer_planes(h) == 3 ? steer_plane_floats(h) : 0;
@@ -820,9 +820,11 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             // CU's 160 KB (2160p: 73.7 + 34.6 KB); else it aliases the
             // exchange buffers (one more barrier per band, and a band's
             // stores cannot overlap the next band's transform)
-            const size_t lx = sizeof(c2) * (size_t)g2 * lds_complex<N>(), ls = sizeof(c2) * (size_t)g2 * h->geo.Hn;
+            // (one column per workgroup, sb_direct: two exchange buffers, no staging)
+            const size_t lx = sizeof(c2) * (size_t)(sb_direct<LOG2N>() ? 2 : g2) * lds_complex<N>(),
+                         ls = sizeof(c2) * (size_t)g2 * t_rows(h->geo.Hn);   // (whole row groups)
             const size_t own_cap = sb_threads<LOG2N>() >= 1024 ? 160 * 1024 : 81920;
-            const int own = h->sb_stg_own && lx + ls <= own_cap ? 1 : 0;
+            const int own = !sb_direct<LOG2N>() && h->sb_stg_own && lx + ls <= own_cap ? 1 : 0;
             hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),
                                lx + (own ? ls : 0), s, h->d_Fb + fstride * (k + f),
                                h->d_T + t_stride * f, band_stride, h->geo, h->spec, h->d_tw, own);

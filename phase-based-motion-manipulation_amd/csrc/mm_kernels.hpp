@@ -1217,7 +1217,16 @@ template <int LOG2N> constexpr int k2_groups()
     return LOG2N >= 13 ? 1 : LOG2N >= 12 ? MM_K2_GROUPS_4K : groups_at_least<LOG2N, MM_K2_GROUPS>();
 }
 // the steerable band-column kernel: two columns per workgroup at every N
-template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, 2>(); }
+// (MM_SB_GPW1 = 1: one column per workgroup where one transform fills a
+// workgroup, N >= 2048, with direct 8-B stores and a double-buffered exchange)
+#ifndef MM_SB_GPW1
+#define MM_SB_GPW1 0
+#endif
+template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, MM_SB_GPW1 ? 1 : 2>(); }
+// k_sb_cols with one column per workgroup: the band loop alternates two
+// exchange buffers (the next band's transform never waits for this one's
+// cross-wave reads) and stores from registers (no staging)
+template <int LOG2N> constexpr bool sb_direct() { return sb_groups<LOG2N>() == 1 && fft_c_v(LOG2N) > 1; }
 template <int LOG2N> constexpr int sb_threads() { return sb_groups<LOG2N>() * fft_T<LOG2N>(); }
 // K2's Q staging buffer (c2 slots written by rows, read back as float4
 // pieces): slot i lives at i ^ (((i >> 4) & 1) << 1), i.e. float4 r at

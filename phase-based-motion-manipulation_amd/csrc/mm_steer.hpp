@@ -91,15 +91,37 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
     }
 }
 
+// Band rows T[b] (k_sb_cols -> k_sb_rows), t_rows(Hn) x N complex per band.
+// MM_SB_RROWS = R: list rows in groups of R, (k, kx) at (k/R) R N + R kx + k%R,
+// so that a workgroup's GPW columns of a row group are one 8 R GPW-byte piece
+// (R = 2, GPW = 2: 32 B, half the lines per store instruction and twice the
+// piece of the row-major layout), and k_sb_rows reads its row at an 8 R-byte
+// stride (the group's other rows are the neighbouring row workgroups', on the
+// same XCD).  R = 1: row-major, (k, kx) at k N + kx.
+#ifndef MM_SB_RROWS
+#define MM_SB_RROWS 2
+#endif
+constexpr int kSbR = MM_SB_RROWS;
+static_assert(kSbR == 1 || kSbR == 2 || kSbR == 4, "MM_SB_RROWS: 1, 2 or 4");
+template <int N> __device__ __forceinline__ size_t t_row(int k)   // offset of (k, 0)
+{
+    return (size_t)(k / kSbR) * (kSbR * N) + k % kSbR;
+}
+constexpr int t_col_stride() { return kSbR; }                     // between (k, kx) and (k, kx+1)
+// rows per band in T (whole row groups)
+__host__ __device__ constexpr int t_rows(int hn) { return (hn + kSbR - 1) / kSbR * kSbR; }
+
 // -------------------------------------------------------------------------
 // Band columns: T[b][k][kx] = IFFT_col(F m_i a_o / N^2)[canvas row rb + k]
 // -------------------------------------------------------------------------
 // GPW >= 2 columns per workgroup (same-XCD blocks own consecutive columns):
-// each band's columns are transposed through LDS and leave as one GPW*8-byte
-// piece per row of the row-major T, which k_sb_rows then reads contiguously
-// (a column-major T made those reads 8-B gathers: 16x L2->L1 traffic).  The
-// band loop issues no loads (twiddle bases hoisted), so its stores are never
-// waited for.
+// each band's columns are transposed through LDS and leave as one
+// 8 R GPW-byte piece per row group of T (t_row), which k_sb_rows then reads
+// row by row (a column-major T made those reads 8-B gathers: 16x L2->L1
+// traffic).  The store piece is what bounds this kernel: 8 B (one column per
+// workgroup) / 16 B (R = 1) / 32 B (R = 2) per lane: C3 O = 8 k_sb_cols 1,020 /
+// 594 / 434 us per frame (profiles/r06h_sb_rows_layout_ab.txt).  The band loop
+// issues no loads (twiddle bases hoisted), so its stores are never waited for.
 #ifndef MM_SB_COLS_WL
 #define MM_SB_COLS_WL 1
 #endif
@@ -110,6 +132,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = sb_groups<LOG2N>();
     constexpr bool SB_WL = MM_SB_COLS_WL && fft_c_v(LOG2N) > 1;
+    constexpr bool DIRECT = SB_WL && sb_direct<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
     const int grp = T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T;
     const int t0 = threadIdx.x % T;
@@ -181,6 +204,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
     // add the angular factor (the same expressions per band: bitwise the
     // band-major loop's values).  The residual band (b = nb) runs last.
     float rm[8];
+    int nbuf = 0;   // DIRECT: exchange buffer of the next band run
     for (int lb = 0; lb <= nb; ++lb) {
         const int i = lb < nb ? 1 + lb / (sp.O / 2) : 0, o = lb < nb ? lb % (sp.O / 2) : 0;
         const int b = lb < nb ? o * nmid + (i - 1) : nb;
@@ -216,6 +240,20 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
             }
             v[j] = scale(v0[j], m);
         }
+        if constexpr (DIRECT) {
+            // one column: rows t + jT leave from registers as 8-B values;
+            // the two exchange buffers alternate, so no barrier guards the
+            // next band's writes against this band's cross-wave reads
+            fft_dit<LOG2N, +1>(v, t, lds_all + nbuf * lds_complex<N>(), wt);
+            nbuf ^= 1;
+            c2 *out = Tb + (size_t)b * band_stride + (size_t)kx * t_col_stride();
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
+                if (valid && k < g.Hn) out[t_row<N>(k)] = v[j];
+            }
+            continue;
+        }
         if constexpr (SB_WL) {
             fft_dit<LOG2N, +1>(v, t, lds, wt);
             // staging over the exchange buffers: every wave past its reads first
@@ -223,14 +261,30 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
         } else {
             fft_regs_w<LOG2N, +1>(v, t, lds, wt);   // ends with a barrier after its last exchange read
         }
+        // staging in T's order: row group m's GPW columns x R rows at m R GPW
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-            if (k < g.Hn) stg[k * GPW + grp] = v[j];
+            if (k < g.Hn) stg[(k / kSbR) * (kSbR * GPW) + kSbR * grp + k % kSbR] = v[j];
         }
         __syncthreads();
         c2 *out = Tb + (size_t)b * band_stride;
-        if constexpr (GPW <= N) {   // whole pieces: GPW / 2 float4 per row
+        const int groups = t_rows(g.Hn) / kSbR;
+        if constexpr (kSbR > 1 && GPW <= N) {   // whole pieces: R GPW / 2 float4 per row group
+            // (a last partial group's missing rows are stale staging, written
+            // to T's pad rows, which k_sb_rows never reads)
+            constexpr int PW = kSbR * GPW / 2;
+            for (int e = grp * T + t; e < groups * PW; e += GPW * T) {
+                const int m = e / PW, part = e - m * PW;
+                *reinterpret_cast<float4 *>(out + (size_t)m * (kSbR * N) + kSbR * kx0 + 2 * part) =
+                    reinterpret_cast<const float4 *>(stg)[e];
+            }
+        } else if constexpr (kSbR > 1) {       // tiny N: fewer columns than groups
+            for (int e = grp * T + t; e < groups * kSbR * GPW; e += GPW * T) {
+                const int m = e / (kSbR * GPW), c = (e / kSbR) % GPW, kk = e % kSbR;
+                if (kx0 + c < N) out[(size_t)m * (kSbR * N) + kSbR * (kx0 + c) + kk] = stg[e];
+            }
+        } else if constexpr (GPW >= 2 && GPW <= N) {   // whole pieces: GPW / 2 float4 per row
             constexpr int PW = GPW / 2;
             for (int e = grp * T + t; e < g.Hn * PW; e += GPW * T) {
                 const int k = e / PW, part = e - k * PW;
@@ -302,10 +356,11 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     c2 v[8];
     float pp[8], puh[8], pul[8];
     auto load_row = [&](int f, int b, int t) {
-        const c2 *row = Tb + (size_t)f * t_stride + (size_t)b * band_stride + (size_t)k * N;
+        const c2 *row = Tb + (size_t)f * t_stride + (size_t)b * band_stride + t_row<N>(k);
 #pragma unroll
         for (int j = 0; j < 8; ++j)   // band_col_zero columns were never written: 0
-            v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp) ? mk(0.0f, 0.0f) : row[t + j * T];
+            v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp) ? mk(0.0f, 0.0f)
+                                                               : row[(t + j * T) * t_col_stride()];
     };
     auto load_state = [&](int b, int t) {
         if (b < nb && !reset) {
