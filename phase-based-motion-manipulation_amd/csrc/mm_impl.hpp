@@ -466,6 +466,11 @@ static int set_attrs(int W)
         for (int f = 0; f < 4; ++f)
             MM_FMT_SWITCH(f, HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rows_inv_compose4<11, FMT_>),
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds)))
+        // k_sb_cols with four columns per workgroup (MM_SB_MIN_GROUPS = 4):
+        // exchange buffers (73.7 KB) + its own staging
+        if constexpr (sb_groups<11>() == 4)
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_cols<11>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
     return MM_OK;
 }
@@ -764,8 +769,10 @@ static int steer_alloc(mm_handle *h, hipStream_t s)
     h->d_sst = nullptr;
     h->steer_nb = -1;
     h->steer_valid = false;
-    // band rows of two frames (k_sb_rows runs frames in pairs)
-    if (h_alloc(h, &h->d_T, sizeof(c2) * 2 * (size_t)(nb + 1) * h->N * t_rows(h->geo.Hn)) != hipSuccess ||
+    // band rows of the frames one k_sb_rows launch runs (pairs; MM_SB_NF=4:
+    // DIFF in fours)
+    if (h_alloc(h, &h->d_T, sizeof(c2) * (h->sb_nf >= 4 ? 4 : 2) * (size_t)(nb + 1) * h->N * t_rows(h->geo.Hn)) !=
+            hipSuccess ||
         h_alloc(h, &h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
@@ -808,7 +815,11 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     // registers (MM_SB_NF=1: one frame per launch)
     const size_t t_stride = band_stride * (size_t)(steer_bands(h) + 1);
     for (int k = 0; k < n;) {
-        const int nf = (h->sb_nf >= 2 && k + 1 < n) ? 2 : 1;
+        // frames of this k_sb_rows launch: 4 (MM_SB_NF=4, DIFF; opt-in: C3
+        // k_sb_rows -1.3 % but k_sb_cols +2.3 %, 1080p k_sb_rows +16 % at 4
+        // waves per SIMD, profiles/r06h_sb_rows_layout_ab.txt), 2 or 1
+        const int nfm = h->sb_nf >= 4 && h->spec.filt != MM_FILTER_IIR ? 4 : h->sb_nf >= 2 ? 2 : 1;
+        const int nf = n - k >= nfm ? nfm : (nfm >= 2 && n - k >= 2 ? 2 : 1);
         const int reset = k < seed;
         for (int f = 0; f < nf; ++f) {
             ProfScope ps(h, s, MM_K_COLS, 0);
@@ -831,7 +842,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             HIPCHK(hipGetLastError());
         }
         // bit f: frame k + f's Yh (the stream's first frame passes through)
-        const int wmask = write ? ((reset ? 0 : 1) | (nf == 2 ? 2 : 0)) : 0;
+        const int wmask = write ? ((reset ? 0 : 1) | ((1 << nf) - 2)) : 0;
         ProfScope ps(h, s, MM_K_ROWS_INV, __builtin_popcount(wmask));
         const dim3 grid((h->geo.Hn + gpw - 1) / gpw), block(wg_threads<LOG2N>());
         float *yh = h->d_Yh + h->yh_stride * k;
@@ -843,7 +854,8 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             if (nf == 2) MM_SB_ROWS(true, 2);
             else MM_SB_ROWS(true, 1);
         } else {
-            if (nf == 2) MM_SB_ROWS(false, 2);
+            if (nf == 4) MM_SB_ROWS(false, 4);
+            else if (nf == 2) MM_SB_ROWS(false, 2);
             else MM_SB_ROWS(false, 1);
         }
 #undef MM_SB_ROWS

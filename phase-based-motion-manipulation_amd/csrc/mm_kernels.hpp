@@ -1222,7 +1222,13 @@ template <int LOG2N> constexpr int k2_groups()
 #ifndef MM_SB_GPW1
 #define MM_SB_GPW1 0
 #endif
-template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, MM_SB_GPW1 ? 1 : 2>(); }
+// (MM_SB_MIN_GROUPS = 4: four columns per workgroup at N = 2048, 64-B pieces:
+// 1080p O = 8 k_sb_cols 90 -> 130 us per frame, one 1,024-thread workgroup
+// per CU in two rounds; profiles/r06h_sb_rows_layout_ab.txt)
+#ifndef MM_SB_MIN_GROUPS
+#define MM_SB_MIN_GROUPS 2
+#endif
+template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, MM_SB_GPW1 ? 1 : MM_SB_MIN_GROUPS>(); }
 // k_sb_cols with one column per workgroup: the band loop alternates two
 // exchange buffers (the next band's transform never waits for this one's
 // cross-wave reads) and stores from registers (no staging)

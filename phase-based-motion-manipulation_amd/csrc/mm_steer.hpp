@@ -330,7 +330,7 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 // frame: it seeds the state and passes through); write_mask bit f: frame f's
 // Yh is wanted.
 template <int LOG2N, bool IIR, int NF>
-__global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR ? 4 : 5)))
+__global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR || NF > 2 ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restrict__ Yh, size_t yh_stride,
                float *st_phi, float *st_uh, float *st_ul,
                int reset, int write_mask, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
