@@ -833,7 +833,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             // stores cannot overlap the next band's transform)
             // (one column per workgroup, sb_direct: two exchange buffers, no staging)
             const size_t lx = sizeof(c2) * (size_t)(sb_direct<LOG2N>() ? 2 : g2) * lds_complex<N>(),
-                         ls = sizeof(c2) * (size_t)g2 * t_rows(h->geo.Hn);   // (whole row groups)
+                         ls = sizeof(c2) * (size_t)g2 * sb_stg_stride(h->geo.Hn, N);   // (whole row groups)
             const size_t own_cap = sb_threads<LOG2N>() >= 1024 ? 160 * 1024 : 81920;
             const int own = !sb_direct<LOG2N>() && h->sb_stg_own && lx + ls <= own_cap ? 1 : 0;
             hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),

@@ -110,6 +110,20 @@ template <int N> __device__ __forceinline__ size_t t_row(int k)   // offset of (
 constexpr int t_col_stride() { return kSbR; }                     // between (k, kx) and (k, kx+1)
 // rows per band in T (whole row groups)
 __host__ __device__ constexpr int t_rows(int hn) { return (hn + kSbR - 1) / kSbR * kSbR; }
+// k_sb_cols staging: column c's rows at c S + k (MM_SB_STG_CM = 1), S = the
+// rows rounded up to 16 mod 32 entries from N = 1024 on: the rows' 8-B
+// writes (16 consecutive rows per lane group) are conflict-free, and so are
+// the float4 reads of a row group's columns (S 2 = 32 mod 64 dwords puts
+// column 1 on the other half of the banks; tools/lds_banks.py "sb_stg").
+// MM_SB_STG_CM = 0: row-group-major (k / R) R GPW + R c + k % R (2-way
+// conflicted writes).
+#ifndef MM_SB_STG_CM
+#define MM_SB_STG_CM 1
+#endif
+__host__ __device__ constexpr int sb_stg_stride(int hn, int n)
+{
+    return MM_SB_STG_CM && n >= 1024 ? (t_rows(hn) + 15) / 32 * 32 + 16 : t_rows(hn);
+}
 
 // -------------------------------------------------------------------------
 // Band columns: T[b][k][kx] = IFFT_col(F m_i a_o / N^2)[canvas row rb + k]
@@ -263,16 +277,34 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
         } else {
             fft_regs_w<LOG2N, +1>(v, t, lds, wt);   // ends with a barrier after its last exchange read
         }
-        // staging in T's order: row group m's GPW columns x R rows at m R GPW
+        // staging: column-major (c S + k, MM_SB_STG_CM) or in T's order (row
+        // group m's GPW columns x R rows at m R GPW)
+        const int S = sb_stg_stride(g.Hn, N);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = (t + j * T - g.rb + 2 * N) & (N - 1);
-            if (k < g.Hn) stg[(k / kSbR) * (kSbR * GPW) + kSbR * grp + k % kSbR] = v[j];
+            if (k < g.Hn)
+                stg[MM_SB_STG_CM ? grp * S + k : (k / kSbR) * (kSbR * GPW) + kSbR * grp + k % kSbR] = v[j];
         }
         __syncthreads();
         c2 *out = Tb + (size_t)b * band_stride;
         const int groups = t_rows(g.Hn) / kSbR;
-        if constexpr (kSbR > 1 && GPW <= N) {   // whole pieces: R GPW / 2 float4 per row group
+        if constexpr (MM_SB_STG_CM && kSbR > 1 && GPW <= N) {   // R GPW / 2 float4 per row group
+            // float4 q of row group m: column q / (R/2), rows 2 (q % (R/2)) ..
+            // +1 of the group (a last partial group's missing rows are stale
+            // staging, written to T's pad rows, which k_sb_rows never reads)
+            constexpr int PW = kSbR * GPW / 2, H2 = kSbR / 2;
+            for (int e = grp * T + t; e < groups * PW; e += GPW * T) {
+                const int m = e / PW, q = e - m * PW, c = q / H2, h = q - c * H2;
+                *reinterpret_cast<float4 *>(out + (size_t)m * (kSbR * N) + kSbR * kx0 + 2 * q) =
+                    *reinterpret_cast<const float4 *>(stg + c * S + m * kSbR + 2 * h);
+            }
+        } else if constexpr (MM_SB_STG_CM) {    // R = 1, or tiny N (fewer columns than groups)
+            for (int e = grp * T + t; e < groups * kSbR * GPW; e += GPW * T) {
+                const int m = e / (kSbR * GPW), o = e - m * (kSbR * GPW), c = o / kSbR, kk = o - c * kSbR;
+                if (kx0 + c < N) out[(size_t)m * (kSbR * N) + kSbR * (kx0 + c) + kk] = stg[c * S + m * kSbR + kk];
+            }
+        } else if constexpr (kSbR > 1 && GPW <= N) {   // whole pieces: R GPW / 2 float4 per row group
             // (a last partial group's missing rows are stale staging, written
             // to T's pad rows, which k_sb_rows never reads)
             constexpr int PW = kSbR * GPW / 2;

@@ -132,6 +132,22 @@ def main():
         report(f"K2 Q staging read float4 swizzled (+{off})", "read_b128",
                [[4 * swz4(64 * w + l + off) for l in lanes] for w in range(GPW * T // 64)])
 
+    # k_sb_cols staging at R = 2, GPW = 2 (1080p Hn = 1084; the read pattern
+    # repeats every 32 row groups): row-group-major vs column-major at stride S
+    rb, Hn = 482, 1084
+    S = (Hn + 1) // 2 * 2
+    S = (S + 15) // 32 * 32 + 16
+    kk = lambda t, j: (t + j * T - rb) % N
+    for g_ in (0, 1):
+        report(f"sb_stg write row-group-major, column {g_}", "write_b64",
+               [[2 * ((kk(64 * w + l, j) // 2) * 4 + 2 * g_ + kk(64 * w + l, j) % 2) for l in lanes]
+                for w in waves for j in range(8)])
+        report(f"sb_stg write column-major S = {S}, column {g_}", "write_b64",
+               [[2 * (g_ * S + kk(64 * w + l, j)) for l in lanes] for w in waves for j in range(8)])
+    report("sb_stg read float4 row-group-major", "read_b128", [[4 * (64 * w + l) for l in lanes] for w in range(8)])
+    report(f"sb_stg read float4 column-major S = {S}", "read_b128",
+           [[2 * ((e % 2) * S + 2 * (e // 2)) for e in (64 * w + l for l in lanes)] for w in range(8)])
+
 
 if __name__ == "__main__":
     main()
