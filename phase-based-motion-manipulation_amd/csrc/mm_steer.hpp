@@ -363,6 +363,9 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 // its Yh at Yh + f * yh_stride; reset applies to frame 0 (the stream's first
 // frame: it seeds the state and passes through); write_mask bit f: frame f's
 // Yh is wanted.
+#ifndef MM_SB_OFF32
+#define MM_SB_OFF32 1
+#endif
 template <int LOG2N, bool IIR, int NF>
 __global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR || NF > 2 ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restrict__ Yh, size_t yh_stride,
@@ -390,11 +393,15 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     c2 v[8];
     float pp[8], puh[8], pul[8];
     auto load_row = [&](int f, int b, int t) {
+        // (row base per workgroup, 32-bit lane offsets: no 64-bit address
+        // math per element, MM_SB_OFF32)
         const c2 *row = Tb + (size_t)f * t_stride + (size_t)b * band_stride + t_row<N>(k);
 #pragma unroll
         for (int j = 0; j < 8; ++j)   // band_col_zero columns were never written: 0
-            v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp) ? mk(0.0f, 0.0f)
-                                                               : row[(t + j * T) * t_col_stride()];
+            v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp)
+                       ? mk(0.0f, 0.0f)
+                       : (MM_SB_OFF32 ? ld_off<c2>(row, (unsigned)((t + j * T) * t_col_stride()) * 8u)
+                                      : row[(t + j * T) * t_col_stride()]);
     };
     auto load_state = [&](int b, int t) {
         if (b < nb && !reset) {
@@ -402,10 +409,18 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int xi = min((t + j * T - xs + N) & (N - 1), Wc - 1);
-                pp[j] = st_phi[rs + xi];
-                if (iir) {
-                    puh[j] = st_uh[rs + xi];
-                    pul[j] = st_ul[rs + xi];
+                if (MM_SB_OFF32) {
+                    pp[j] = ld_off<float>(st_phi + rs, (unsigned)xi * 4u);
+                    if (iir) {
+                        puh[j] = ld_off<float>(st_uh + rs, (unsigned)xi * 4u);
+                        pul[j] = ld_off<float>(st_ul + rs, (unsigned)xi * 4u);
+                    }
+                } else {
+                    pp[j] = st_phi[rs + xi];
+                    if (iir) {
+                        puh[j] = st_uh[rs + xi];
+                        pul[j] = st_ul[rs + xi];
+                    }
                 }
             }
         }
@@ -498,10 +513,18 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
                 for (int j = 0; j < 8; ++j) {
                     const int xi = (t + j * T - xs + N) & (N - 1);
                     if (xi < Wc) {
-                        st_phi[rs + xi] = nph[j];
-                        if (iir) {
-                            st_uh[rs + xi] = nuh[j];
-                            st_ul[rs + xi] = nul[j];
+                        if (MM_SB_OFF32) {
+                            st_off<float>(st_phi + rs, (unsigned)xi * 4u, nph[j]);
+                            if (iir) {
+                                st_off<float>(st_uh + rs, (unsigned)xi * 4u, nuh[j]);
+                                st_off<float>(st_ul + rs, (unsigned)xi * 4u, nul[j]);
+                            }
+                        } else {
+                            st_phi[rs + xi] = nph[j];
+                            if (iir) {
+                                st_uh[rs + xi] = nuh[j];
+                                st_ul[rs + xi] = nul[j];
+                            }
                         }
                     }
                 }
