@@ -821,7 +821,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         const int nfm = h->sb_nf >= 4 && h->spec.filt != MM_FILTER_IIR ? 4 : h->sb_nf >= 2 ? 2 : 1;
         const int nf = n - k >= nfm ? nfm : (nfm >= 2 && n - k >= 2 ? 2 : 1);
         const int reset = k < seed;
-        for (int f = 0; f < nf; ++f) {
+        {   // the band columns of the group's nf frames, one launch (blockIdx.y: frame)
             ProfScope ps(h, s, MM_K_COLS, 0);
             const int g2 = sb_groups<LOG2N>();
             // the staging [Hn][GPW] gets its own LDS area where it costs no
@@ -836,10 +836,17 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
                          ls = sizeof(c2) * (size_t)g2 * sb_stg_stride(h->geo.Hn, N);   // (whole row groups)
             const size_t own_cap = sb_threads<LOG2N>() >= 1024 ? 160 * 1024 : 81920;
             const int own = !sb_direct<LOG2N>() && h->sb_stg_own && lx + ls <= own_cap ? 1 : 0;
-            hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2), dim3(sb_threads<LOG2N>()),
-                               lx + (own ? ls : 0), s, h->d_Fb + fstride * (k + f),
-                               h->d_T + t_stride * f, band_stride, h->geo, h->spec, h->d_tw, own);
-            HIPCHK(hipGetLastError());
+            // one launch for the group's frames at N <= 2048 (1080p O = 8 DIFF
+            // 5.33k -> 5.53k frames/s: half the kernel boundaries); per frame
+            // at N = 4096, whose 2,048-workgroup launches gain nothing from it
+            // (C3 k_sb_cols 424 -> 430 us; profiles/r06h_sb_rows_layout_ab.txt)
+            const int per = LOG2N >= 12 ? 1 : nf;
+            for (int f = 0; f < nf; f += per) {
+                hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2, per), dim3(sb_threads<LOG2N>()),
+                                   lx + (own ? ls : 0), s, h->d_Fb + fstride * (k + f), h->d_T + t_stride * f,
+                                   band_stride, h->geo, h->spec, h->d_tw, own, fstride, t_stride);
+                HIPCHK(hipGetLastError());
+            }
         }
         // bit f: frame k + f's Yh (the stream's first frame passes through)
         const int wmask = write ? ((reset ? 0 : 1) | ((1 << nf) - 2)) : 0;

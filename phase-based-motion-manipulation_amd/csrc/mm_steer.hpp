@@ -142,8 +142,12 @@ __host__ __device__ constexpr int sb_stg_stride(int hn, int n)
 template <int LOG2N>
 __global__ __launch_bounds__(sb_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(4)))
 void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_stride, Geo g, Spec sp,
-               const c2 *__restrict__ tw, int stg_own)
+               const c2 *__restrict__ tw, int stg_own, size_t f_stride, size_t t_stride)
 {
+    // blockIdx.y: the frame of the launch's frames (k_sb_rows' group of NF),
+    // its F at Fb + y f_stride, its band rows at Tb + y t_stride
+    Fb += blockIdx.y * f_stride;
+    Tb += blockIdx.y * t_stride;
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = sb_groups<LOG2N>();
     constexpr bool SB_WL = MM_SB_COLS_WL && fft_c_v(LOG2N) > 1;
     constexpr bool DIRECT = SB_WL && sb_direct<LOG2N>();
