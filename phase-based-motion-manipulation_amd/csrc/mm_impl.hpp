@@ -65,6 +65,7 @@ struct mm_handle {
     int steer_nb;               // bands the steerable buffers were sized for (-1: none)
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
     int sb_nf;                  // frames per k_sb_rows launch (MM_SB_NF; 2: pairs)
+    int sb_cf;                  // frames per k_sb_cols launch at N <= 2048 (MM_SB_CF)
     bool sb_stg_own;            // k_sb_cols stages in its own LDS area where it fits (MM_SB_STG)
     bool steer_valid;           // d_sst holds the state after the previous frame
     // G: chunk + 1 slots of K1's row spectra.  Slot gs holds G_{t-1}, the row
@@ -753,6 +754,11 @@ static size_t steer_state_bytes(const mm_handle *h)
 // Band buffers and the temporal state planes for the current levels and
 // orientations.  Reallocated (state invalid) only when those change, never
 // by mm_set_batch: the per-batch spectra Fb grow separately (ensure_frames).
+// frames of one k_sb_cols launch chunk (MM_SB_CF; per-frame launches at N = 4096)
+static int sb_cols_frames(const mm_handle *h)
+{
+    return h->N >= 4096 ? 2 : std::max(2, h->sb_cf);
+}
 static int steer_alloc(mm_handle *h, hipStream_t s)
 {
     const int nb = steer_bands(h);
@@ -769,10 +775,10 @@ static int steer_alloc(mm_handle *h, hipStream_t s)
     h->d_sst = nullptr;
     h->steer_nb = -1;
     h->steer_valid = false;
-    // band rows of the frames one k_sb_rows launch runs (pairs; MM_SB_NF=4:
-    // DIFF in fours)
-    if (h_alloc(h, &h->d_T, sizeof(c2) * (h->sb_nf >= 4 ? 4 : 2) * (size_t)(nb + 1) * h->N * t_rows(h->geo.Hn)) !=
-            hipSuccess ||
+    // band rows of the frames one k_sb_cols launch chunk covers (sb_cols_frames;
+    // at least the k_sb_rows group: pairs, MM_SB_NF=4: DIFF in fours)
+    const int tfr = std::max(sb_cols_frames(h), h->sb_nf >= 4 ? 4 : 2);
+    if (h_alloc(h, &h->d_T, sizeof(c2) * tfr * (size_t)(nb + 1) * h->N * t_rows(h->geo.Hn)) != hipSuccess ||
         h_alloc(h, &h->d_sst, steer_state_bytes(h) + sizeof(float)) != hipSuccess)
         return MM_ERR_OOM;
     h->steer_nb = nb;
@@ -814,14 +820,21 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
     // whose workgroups carry the first frame's new state to the second in
     // registers (MM_SB_NF=1: one frame per launch)
     const size_t t_stride = band_stride * (size_t)(steer_bands(h) + 1);
-    for (int k = 0; k < n;) {
-        // frames of this k_sb_rows launch: 4 (MM_SB_NF=4, DIFF; opt-in: C3
-        // k_sb_rows -1.3 % but k_sb_cols +2.3 %, 1080p k_sb_rows +16 % at 4
-        // waves per SIMD, profiles/r06h_sb_rows_layout_ab.txt), 2 or 1
-        const int nfm = h->sb_nf >= 4 && h->spec.filt != MM_FILTER_IIR ? 4 : h->sb_nf >= 2 ? 2 : 1;
-        const int nf = n - k >= nfm ? nfm : (nfm >= 2 && n - k >= 2 ? 2 : 1);
-        const int reset = k < seed;
-        {   // the band columns of the group's nf frames, one launch (blockIdx.y: frame)
+    // frames of this k_sb_rows launch: 4 (MM_SB_NF=4, DIFF; opt-in: C3
+    // k_sb_rows -1.3 % but k_sb_cols +2.3 %, 1080p k_sb_rows +16 % at 4
+    // waves per SIMD, profiles/r06h_sb_rows_layout_ab.txt), 2 or 1
+    const int nfm = h->sb_nf >= 4 && h->spec.filt != MM_FILTER_IIR ? 4 : h->sb_nf >= 2 ? 2 : 1;
+    // k_sb_cols runs the band columns of sb_cf (MM_SB_CF, default 8) frames per
+    // launch at N <= 2048 (blockIdx.y: frame), then the chunk's k_sb_rows
+    // groups: the kernel boundaries are what it saves (1080p O = 8 DIFF, same
+    // call: 1 / 2 / 4 / 8 frames per launch 5.33k / 5.54k / 5.64k / 5.67k
+    // frames/s; 1.85 GB of band rows at 8); per frame at N = 4096, whose
+    // 2,048-workgroup launches gain nothing from it (C3 k_sb_cols 424 -> 430
+    // us at 2; profiles/r06h_sb_rows_layout_ab.txt)
+    const int cf = std::max(sb_cols_frames(h), nfm);
+    for (int c0 = 0; c0 < n; c0 += cf) {
+        const int cn = std::min(cf, n - c0);
+        {
             ProfScope ps(h, s, MM_K_COLS, 0);
             const int g2 = sb_groups<LOG2N>();
             // the staging [Hn][GPW] gets its own LDS area where it costs no
@@ -836,38 +849,40 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
                          ls = sizeof(c2) * (size_t)g2 * sb_stg_stride(h->geo.Hn, N);   // (whole row groups)
             const size_t own_cap = sb_threads<LOG2N>() >= 1024 ? 160 * 1024 : 81920;
             const int own = !sb_direct<LOG2N>() && h->sb_stg_own && lx + ls <= own_cap ? 1 : 0;
-            // one launch for the group's frames at N <= 2048 (1080p O = 8 DIFF
-            // 5.33k -> 5.53k frames/s: half the kernel boundaries); per frame
-            // at N = 4096, whose 2,048-workgroup launches gain nothing from it
-            // (C3 k_sb_cols 424 -> 430 us; profiles/r06h_sb_rows_layout_ab.txt)
-            const int per = LOG2N >= 12 ? 1 : nf;
-            for (int f = 0; f < nf; f += per) {
+            const int per = LOG2N >= 12 ? 1 : cn;
+            for (int f = 0; f < cn; f += per) {
                 hipLaunchKernelGGL((k_sb_cols<LOG2N>), dim3((N + g2 - 1) / g2, per), dim3(sb_threads<LOG2N>()),
-                                   lx + (own ? ls : 0), s, h->d_Fb + fstride * (k + f), h->d_T + t_stride * f,
+                                   lx + (own ? ls : 0), s, h->d_Fb + fstride * (c0 + f), h->d_T + t_stride * f,
                                    band_stride, h->geo, h->spec, h->d_tw, own, fstride, t_stride);
                 HIPCHK(hipGetLastError());
             }
         }
-        // bit f: frame k + f's Yh (the stream's first frame passes through)
-        const int wmask = write ? ((reset ? 0 : 1) | ((1 << nf) - 2)) : 0;
-        ProfScope ps(h, s, MM_K_ROWS_INV, __builtin_popcount(wmask));
-        const dim3 grid((h->geo.Hn + gpw - 1) / gpw), block(wg_threads<LOG2N>());
-        float *yh = h->d_Yh + h->yh_stride * k;
+        for (int k = c0; k < c0 + cn;) {
+            const int left = c0 + cn - k;
+            const int nf = left >= nfm ? nfm : (nfm >= 2 && left >= 2 ? 2 : 1);
+            const int reset = k < seed;
+            // bit f: frame k + f's Yh (the stream's first frame passes through)
+            const int wmask = write ? ((reset ? 0 : 1) | ((1 << nf) - 2)) : 0;
+            ProfScope ps(h, s, MM_K_ROWS_INV, __builtin_popcount(wmask));
+            const dim3 grid((h->geo.Hn + gpw - 1) / gpw), block(wg_threads<LOG2N>());
+            float *yh = h->d_Yh + h->yh_stride * k;
+            c2 *tk = h->d_T + t_stride * (k - c0);
 #define MM_SB_ROWS(IIRV, NFV)                                                                              \
-        hipLaunchKernelGGL((k_sb_rows<LOG2N, IIRV, NFV>), grid, block, lds, s, h->d_T, band_stride, t_stride, \
-                           yh, h->yh_stride, sst, sst + plane, sst + 2 * plane, reset, wmask, h->geo, h->spec, \
-                           h->blur, h->d_tw)
-        if (h->spec.filt == MM_FILTER_IIR) {
-            if (nf == 2) MM_SB_ROWS(true, 2);
-            else MM_SB_ROWS(true, 1);
-        } else {
-            if (nf == 4) MM_SB_ROWS(false, 4);
-            else if (nf == 2) MM_SB_ROWS(false, 2);
-            else MM_SB_ROWS(false, 1);
-        }
+            hipLaunchKernelGGL((k_sb_rows<LOG2N, IIRV, NFV>), grid, block, lds, s, tk, band_stride, t_stride, \
+                               yh, h->yh_stride, sst, sst + plane, sst + 2 * plane, reset, wmask, h->geo,   \
+                               h->spec, h->blur, h->d_tw)
+            if (h->spec.filt == MM_FILTER_IIR) {
+                if (nf == 2) MM_SB_ROWS(true, 2);
+                else MM_SB_ROWS(true, 1);
+            } else {
+                if (nf == 4) MM_SB_ROWS(false, 4);
+                else if (nf == 2) MM_SB_ROWS(false, 2);
+                else MM_SB_ROWS(false, 1);
+            }
 #undef MM_SB_ROWS
-        HIPCHK(hipGetLastError());
-        k += nf;
+            HIPCHK(hipGetLastError());
+            k += nf;
+        }
     }
     if (sst == h->d_sst) h->steer_valid = true;
     const size_t fb = (size_t)h->W * h->H * fmt_bpp(fmt);

@@ -165,41 +165,46 @@ def test_gpu_chunked_and_state_handoff(W, H):
 @pytest.mark.gpu
 @pytest.mark.parametrize("filt", [0, 1])
 def test_gpu_frames_per_launch_bitwise(filt):
-    """k_sb_rows runs 1 or 2 frames per launch (MM_SB_NF, read at mm_create),
-    carrying the band state from the first to the second in registers: the
-    same expressions in the same order, so the outputs and the final state are
-    bitwise equal for both groupings, including a batch (7) that leaves a
-    single frame."""
+    """k_sb_rows runs 1, 2 or (DIFF) 4 frames per launch (MM_SB_NF, read at
+    mm_create), carrying the band state from one frame to the next in
+    registers, and k_sb_cols the band columns of MM_SB_CF frames per launch:
+    the same expressions in the same order, so the outputs and the final state
+    are bitwise equal for every grouping, including batches (11 of 13 frames)
+    whose column chunks (8 + 3, 2 + 1) leave a pair and a single frame."""
     import os
     import mm355
     import torch
-    W, H, n = 200, 120, 9
+    W, H, n = 200, 120, 13
     fr = frames(W, H, n)
     dev = torch.from_numpy(np.stack(fr)).cuda()
     p = mm355.Params.make(levels=5, phase_scale=10.0, mode=mm355.MODE_STEERABLE,
                           orientations=8, temporal_filter=filt)
+    combos = [("1", "2"), ("2", "2"), ("2", "8"), ("2", "4")] + ([("4", "8")] if filt == 0 else [])
     res = {}
-    old = os.environ.get("MM_SB_NF")
+    old = {k: os.environ.get(k) for k in ("MM_SB_NF", "MM_SB_CF")}
     try:
-        for nf in ("1", "2"):
+        for nf, cf in combos:
             os.environ["MM_SB_NF"] = nf
+            os.environ["MM_SB_CF"] = cf
             h = mm355.Handle(W, H, p)
-            h.set_batch(7)
+            h.set_batch(11)
             out = torch.empty_like(dev)
             h.process_stream(dev, out, n, mm355.RGBA32F)
             st = torch.empty(h.state_bytes, dtype=torch.uint8, device="cuda")
             h.get_state(st)
             torch.cuda.synchronize()
-            res[nf] = (out.cpu(), st.cpu())
+            res[(nf, cf)] = (out.cpu(), st.cpu())
             h.close()
     finally:
-        if old is None:
-            os.environ.pop("MM_SB_NF", None)
-        else:
-            os.environ["MM_SB_NF"] = old
-    for nf in ("2",):
-        assert torch.equal(res[nf][0], res["1"][0]), nf
-        assert torch.equal(res[nf][1], res["1"][1]), nf
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    ref = res[("1", "2")]
+    for c in combos[1:]:
+        assert torch.equal(res[c][0], ref[0]), c
+        assert torch.equal(res[c][1], ref[1]), c
 
 
 @pytest.mark.gpu
