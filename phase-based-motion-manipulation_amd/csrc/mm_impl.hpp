@@ -66,6 +66,7 @@ struct mm_handle {
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
     int sb_nf;                  // frames per k_sb_rows launch (MM_SB_NF; 2: pairs)
     int sb_cf;                  // frames per k_sb_cols launch at N <= 2048 (MM_SB_CF)
+    int sb_rg;                  // k_sb_rows: a chunk's frame groups in one launch (MM_SB_RG)
     bool sb_stg_own;            // k_sb_cols stages in its own LDS area where it fits (MM_SB_STG)
     bool steer_valid;           // d_sst holds the state after the previous frame
     // G: chunk + 1 slots of K1's row spectra.  Slot gs holds G_{t-1}, the row
@@ -860,9 +861,13 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
         for (int k = c0; k < c0 + cn;) {
             const int left = c0 + cn - k;
             const int nf = left >= nfm ? nfm : (nfm >= 2 && left >= 2 ? 2 : 1);
+            // the chunk's whole groups of nf frames in one launch, each
+            // workgroup running them one after the other (MM_SB_RG=0: a launch
+            // per group)
+            const int ng = h->sb_rg && h->spec.filt != MM_FILTER_IIR ? left / nf : 1;
             const int reset = k < seed;
             // bit f: frame k + f's Yh (the stream's first frame passes through)
-            const int wmask = write ? ((reset ? 0 : 1) | ((1 << nf) - 2)) : 0;
+            const int wmask = write ? (((1 << (ng * nf)) - 1) & ~(reset ? 1 : 0)) : 0;
             ProfScope ps(h, s, MM_K_ROWS_INV, __builtin_popcount(wmask));
             const dim3 grid((h->geo.Hn + gpw - 1) / gpw), block(wg_threads<LOG2N>());
             float *yh = h->d_Yh + h->yh_stride * k;
@@ -870,7 +875,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
 #define MM_SB_ROWS(IIRV, NFV)                                                                              \
             hipLaunchKernelGGL((k_sb_rows<LOG2N, IIRV, NFV>), grid, block, lds, s, tk, band_stride, t_stride, \
                                yh, h->yh_stride, sst, sst + plane, sst + 2 * plane, reset, wmask, h->geo,   \
-                               h->spec, h->blur, h->d_tw)
+                               h->spec, h->blur, h->d_tw, ng)
             if (h->spec.filt == MM_FILTER_IIR) {
                 if (nf == 2) MM_SB_ROWS(true, 2);
                 else MM_SB_ROWS(true, 1);
@@ -881,7 +886,7 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             }
 #undef MM_SB_ROWS
             HIPCHK(hipGetLastError());
-            k += nf;
+            k += ng * nf;
         }
     }
     if (sst == h->d_sst) h->steer_valid = true;

@@ -374,7 +374,7 @@ template <int LOG2N, bool IIR, int NF>
 __global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR || NF > 2 ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restrict__ Yh, size_t yh_stride,
                float *st_phi, float *st_uh, float *st_ul,
-               int reset, int write_mask, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw)
+               int reset, int write_mask, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw, int ngroups)
 {
     constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
@@ -396,10 +396,17 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     // row k of band b of frame f (contiguous) and its state: loaded one row ahead
     c2 v[8];
     float pp[8], puh[8], pul[8];
+    // ngroups groups of NF frames per launch, one after the other in every
+    // workgroup (its row's state goes to memory between groups and comes back
+    // to the same lanes): fewer kernel boundaries than a launch per group.
+    // Group gi: band rows at Tb + gi NF t_stride, Yh at Yh + gi NF yh_stride,
+    // write_mask bits gi NF .., reset for group 0 only.
+    const c2 *Tg = Tb;
+    int rz = reset;
     auto load_row = [&](int f, int b, int t) {
         // (row base per workgroup, 32-bit lane offsets: no 64-bit address
         // math per element, MM_SB_OFF32)
-        const c2 *row = Tb + (size_t)f * t_stride + (size_t)b * band_stride + t_row<N>(k);
+        const c2 *row = Tg + (size_t)f * t_stride + (size_t)b * band_stride + t_row<N>(k);
 #pragma unroll
         for (int j = 0; j < 8; ++j)   // band_col_zero columns were never written: 0
             v[j] = band_col_zero<N>(b, nb, nmid, t + j * T, sp)
@@ -408,7 +415,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
                                       : row[(t + j * T) * t_col_stride()]);
     };
     auto load_state = [&](int b, int t) {
-        if (b < nb && !reset) {
+        if (b < nb && !rz) {
             const size_t rs = ((size_t)b * g.Hn + k) * Wc;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -429,6 +436,15 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
             }
         }
     };
+    // (IIR: one group per launch; its three state planes leave no registers
+    // for the loop: 34 B of spills inside the band loop, k_sb_rows +6 %)
+    const int ngr = IIR ? 1 : ngroups;
+    for (int gi = 0; gi < ngr; ++gi) {
+    Tg = Tb + (size_t)gi * NF * t_stride;
+    rz = gi == 0 ? reset : 0;
+    const int wmask = write_mask >> (gi * NF);
+    float *Yg = Yh + (size_t)gi * NF * yh_stride;
+    if (gi > 0) __syncthreads();   // the previous group's blur reads of the LDS are done
     {
         int t = t0;
         asm volatile("" : "+v"(t));
@@ -459,8 +475,8 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
                 continue;
             }
             // this band's new state and amplified synthesis, in registers
-            const bool rst = f == 0 && reset;            // the stream's first frame
-            const bool wr = ((write_mask >> f) & 1) != 0;
+            const bool rst = f == 0 && rz;               // the stream's first frame
+            const bool wr = ((wmask >> f) & 1) != 0;
             float nph[8], nuh[8], nul[8];
             // local phases two bins at a time (packed FP32, fast_atan2's values)
             float phs[8];
@@ -542,13 +558,13 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     const bool interior = g.x0 >= 2 && g.x0 + g.Wy + 2 <= N;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-        if (!((write_mask >> f) & 1)) continue;   // uniform
+        if (!((wmask >> f) & 1)) continue;        // uniform
         if (f > 0) __syncthreads();               // the previous frame's blur reads are done
 #pragma unroll
         for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[f][j]);
         __syncthreads();
         if (valid) {
-            float *out = Yh + (size_t)f * yh_stride + (size_t)k * g.Wy;
+            float *out = Yg + (size_t)f * yh_stride + (size_t)k * g.Wy;
             for (int X = t0; X < g.Wy; X += T) {
                 const int c = g.x0 + X;
                 float acc;
@@ -563,6 +579,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
             }
         }
     }
+    }   // groups
 }
 
 }  // namespace mm
