@@ -755,10 +755,11 @@ static size_t steer_state_bytes(const mm_handle *h)
 // Band buffers and the temporal state planes for the current levels and
 // orientations.  Reallocated (state invalid) only when those change, never
 // by mm_set_batch: the per-batch spectra Fb grow separately (ensure_frames).
-// frames of one k_sb_cols launch chunk (MM_SB_CF; per-frame launches at N = 4096)
+// frames of one k_sb_cols launch chunk (MM_SB_CF, 2 .. 16: k_sb_rows' write
+// mask holds a bit per frame of its launch; per-frame launches at N = 4096)
 static int sb_cols_frames(const mm_handle *h)
 {
-    return h->N >= 4096 ? 2 : std::max(2, h->sb_cf);
+    return h->N >= 4096 ? 2 : std::min(16, std::max(2, h->sb_cf));
 }
 static int steer_alloc(mm_handle *h, hipStream_t s)
 {
