@@ -370,6 +370,9 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 #ifndef MM_SB_OFF32
 #define MM_SB_OFF32 1
 #endif
+#ifndef MM_SB_IIR_GROUPS
+#define MM_SB_IIR_GROUPS 0
+#endif
 template <int LOG2N, bool IIR, int NF>
 __global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR || NF > 2 ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restrict__ Yh, size_t yh_stride,
@@ -438,7 +441,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     };
     // (IIR: one group per launch; its three state planes leave no registers
     // for the loop: 34 B of spills inside the band loop, k_sb_rows +6 %)
-    const int ngr = IIR ? 1 : ngroups;
+    const int ngr = IIR && !MM_SB_IIR_GROUPS ? 1 : ngroups;
     for (int gi = 0; gi < ngr; ++gi) {
     Tg = Tb + (size_t)gi * NF * t_stride;
     rz = gi == 0 ? reset : 0;
@@ -556,16 +559,20 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     // |y| (ConvertComplexMagToTex) then the horizontal half of ApplyAntiAliasing
     float *raw = reinterpret_cast<float *>(lds);
     const bool interior = g.x0 >= 2 && g.x0 + g.Wy + 2 <= N;
+    // (an opaque lane index: the blur's addressing is not hoisted out of the
+    // group loop into registers live across the band loop)
+    int tb = t0;
+    asm volatile("" : "+v"(tb));
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
         if (!((wmask >> f) & 1)) continue;        // uniform
         if (f > 0) __syncthreads();               // the previous frame's blur reads are done
 #pragma unroll
-        for (int j = 0; j < 8; ++j) raw[t0 + j * T] = fabsf(y[f][j]);
+        for (int j = 0; j < 8; ++j) raw[tb + j * T] = fabsf(y[f][j]);
         __syncthreads();
         if (valid) {
             float *out = Yg + (size_t)f * yh_stride + (size_t)k * g.Wy;
-            for (int X = t0; X < g.Wy; X += T) {
+            for (int X = tb; X < g.Wy; X += T) {
                 const int c = g.x0 + X;
                 float acc;
                 if (interior) {
