@@ -298,6 +298,7 @@ int mm_create(int width, int height, const mm_params *p, int hip_device, mm_hand
     h->k34_oneshot = getenv("MM_K34_ONESHOT") ? atoi(getenv("MM_K34_ONESHOT")) : 1;
     h->sb_nf = getenv("MM_SB_NF") ? atoi(getenv("MM_SB_NF")) : 2;
     h->sb_cf = getenv("MM_SB_CF") ? atoi(getenv("MM_SB_CF")) : 8;
+    h->sb_cf4k = getenv("MM_SB_CF4K") ? atoi(getenv("MM_SB_CF4K")) : 2;
     h->sb_rg = getenv("MM_SB_RG") ? atoi(getenv("MM_SB_RG")) != 0 : true;
     h->sb_stg_own = getenv("MM_SB_STG") ? atoi(getenv("MM_SB_STG")) != 0 : true;
 

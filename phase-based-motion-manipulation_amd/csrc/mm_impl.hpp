@@ -66,6 +66,7 @@ struct mm_handle {
     int steer_planes;           // state planes allocated (1: DIFF, 3: IIR)
     int sb_nf;                  // frames per k_sb_rows launch (MM_SB_NF; 2: pairs)
     int sb_cf;                  // frames per k_sb_cols launch at N <= 2048 (MM_SB_CF)
+    int sb_cf4k;                // frames per column chunk at N = 4096 (MM_SB_CF4K; launches stay per frame)
     int sb_rg;                  // k_sb_rows: a chunk's frame groups in one launch (MM_SB_RG)
     bool sb_stg_own;            // k_sb_cols stages in its own LDS area where it fits (MM_SB_STG)
     bool steer_valid;           // d_sst holds the state after the previous frame
@@ -759,7 +760,7 @@ static size_t steer_state_bytes(const mm_handle *h)
 // mask holds a bit per frame of its launch; per-frame launches at N = 4096)
 static int sb_cols_frames(const mm_handle *h)
 {
-    return h->N >= 4096 ? 2 : std::min(16, std::max(2, h->sb_cf));
+    return std::min(16, std::max(2, h->N >= 4096 ? h->sb_cf4k : h->sb_cf));
 }
 static int steer_alloc(mm_handle *h, hipStream_t s)
 {
