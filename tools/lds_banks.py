@@ -217,3 +217,49 @@ def k34_report(N=2048, x0=64):
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "k34":
     k34_report(int(sys.argv[1]))
+
+
+def xpad(i, ns):
+    """mm_fft.hpp xpad for the wave-local 512-point inner transform (LOG2N 9)."""
+    s, a = (3, 1) if ns == 1 else ((5, 4) if ns == 8 else (30, 0))
+    return i + a * (i >> s)
+
+
+def fft_wl_report(N=2048):
+    """The wave-local transform's LDS traffic per wave (fft_dif / fft_dit at
+    C = N / 512 waves, mm_fft.hpp): the cross-wave exchange, then the inner
+    512-point Stockham passes' two wave-local exchanges (radix 8; pass 0 at
+    Ns = 1 with pad8, pass 1 at Ns = 8 with xpad A = 4, S = 5).  Every K2 / K1
+    / K34 transform runs these, so their sum is the FFT share of a kernel's
+    LDS cycles (tools/lds_banks.py main() covers the tables and staging)."""
+    C = max(N // 512, 1)
+    RS = 512 + 64
+    lanes = range(64)
+    tot = {}
+
+    def rep(name, kind, pats):
+        c = [cycles(kind, [2 * e for e in p]) for p in pats]
+        got, mn = sum(x[0] for x in c), sum(x[1] for x in c) * (GROUPS[kind][2] if kind != "read_b64" else 1)
+        # minimum: each lane group needs width dwords per lane over its banks
+        groups, nb, width = GROUPS[kind]
+        mn = sum(max(1, len(g) * width // nb) for g in groups) * len(pats)
+        tot[name] = (got, mn)
+        print(f"{name:58s} {kind:10s} {got / len(pats):5.2f} cycles/instr (min {mn / len(pats):.0f})")
+
+    if C > 1:
+        H = 8 // C
+        rep("fft_dif cross-wave write lds[m RS + n2]", "write_b64",
+            [[m * RS + (l + 64 * C * h) for l in lanes] for h in range(H) for m in range(C)])
+        rep("fft_dif cross-wave read reg[l + 64 j]", "read_b64", [[l + 64 * j for l in lanes] for j in range(8)])
+    for p_, ns in ((0, 1), (1, 8)):
+        rep(f"inner pass {p_} write (Ns = {ns})", "write_b64",
+            [[xpad((l // ns) * ns * 8 + l % ns + m * ns, ns) for l in lanes] for m in range(8)])
+        rep(f"inner pass {p_} read (Ns = {ns})", "read_b64",
+            [[xpad(l + 64 * j, ns) for l in lanes] for j in range(8)])
+    got = sum(v[0] for v in tot.values())
+    mn = sum(v[1] for v in tot.values())
+    print(f"{'one wave-local transform: LDS cycles / conflict-free minimum':58s} {got} / {mn} = {got / mn:.3f}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "fft":
+    fft_wl_report(int(sys.argv[1]))
