@@ -1216,23 +1216,27 @@ template <int LOG2N> constexpr int k2_groups()
 {
     return LOG2N >= 13 ? 1 : LOG2N >= 12 ? MM_K2_GROUPS_4K : groups_at_least<LOG2N, MM_K2_GROUPS>();
 }
-// the steerable band-column kernel: two columns per workgroup at every N
-// (MM_SB_GPW1 = 1: one column per workgroup where one transform fills a
-// workgroup, N >= 2048, with direct 8-B stores and a double-buffered exchange)
+// the steerable band-column kernel: one column per workgroup where one
+// transform fills a workgroup (N >= 2048), else the transforms a 256-thread
+// workgroup holds; its staged pieces are 32 B through the band rows' row
+// groups of 4 (MM_SB_RROWS, mm_steer.hpp), and the workgroups of a CU run
+// independently (two columns in one 1,024-thread workgroup synchronised 16
+// waves per barrier: C3 O = 8 k_sb_cols 434 -> 380 us, 1080p 81.7 -> 69.4,
+// profiles/r06h_sb_rows_layout_ab.txt).  MM_SB_MIN_GROUPS = 2 / 4: two / four
+// columns per workgroup (four at N = 2048: 130 us, one workgroup per CU in
+// two rounds).  MM_SB_GPW1 = 1: one column with direct 8-B stores and a
+// double-buffered exchange (no staging: C3 1,020 us).
 #ifndef MM_SB_GPW1
 #define MM_SB_GPW1 0
 #endif
-// (MM_SB_MIN_GROUPS = 4: four columns per workgroup at N = 2048, 64-B pieces:
-// 1080p O = 8 k_sb_cols 90 -> 130 us per frame, one 1,024-thread workgroup
-// per CU in two rounds; profiles/r06h_sb_rows_layout_ab.txt)
 #ifndef MM_SB_MIN_GROUPS
-#define MM_SB_MIN_GROUPS 2
+#define MM_SB_MIN_GROUPS 1
 #endif
 template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, MM_SB_GPW1 ? 1 : MM_SB_MIN_GROUPS>(); }
 // k_sb_cols with one column per workgroup: the band loop alternates two
 // exchange buffers (the next band's transform never waits for this one's
 // cross-wave reads) and stores from registers (no staging)
-template <int LOG2N> constexpr bool sb_direct() { return sb_groups<LOG2N>() == 1 && fft_c_v(LOG2N) > 1; }
+template <int LOG2N> constexpr bool sb_direct() { return MM_SB_GPW1 && sb_groups<LOG2N>() == 1 && fft_c_v(LOG2N) > 1; }
 template <int LOG2N> constexpr int sb_threads() { return sb_groups<LOG2N>() * fft_T<LOG2N>(); }
 // K2's Q staging buffer (c2 slots written by rows, read back as float4
 // pieces): slot i lives at i ^ (((i >> 4) & 1) << 1), i.e. float4 r at

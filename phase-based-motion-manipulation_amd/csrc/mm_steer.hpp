@@ -94,15 +94,17 @@ void k_cols_fwd(const c2 *__restrict__ G, size_t g_stride, c2 *__restrict__ Fb, 
 // Band rows T[b] (k_sb_cols -> k_sb_rows), t_rows(Hn) x N complex per band.
 // MM_SB_RROWS = R: list rows in groups of R, (k, kx) at (k/R) R N + R kx + k%R,
 // so that a workgroup's GPW columns of a row group are one 8 R GPW-byte piece
-// (R = 2, GPW = 2: 32 B, half the lines per store instruction and twice the
-// piece of the row-major layout), and k_sb_rows reads its row at an 8 R-byte
-// stride (the group's other rows are the neighbouring row workgroups', on the
-// same XCD).  R = 1: row-major, (k, kx) at k N + kx.
+// (R = 4, GPW = 1: 32 B, a quarter of the lines per store instruction and four
+// times the piece of the row-major layout), and k_sb_rows reads its row at an
+// 8 R-byte stride (the group's other rows are the neighbouring row
+// workgroups', on the same XCD).  R = 1: row-major, (k, kx) at k N + kx.
+// Same call (profiles/r06h_sb_rows_layout_ab.txt), C3 O = 8 DIFF frames/s:
+// R 1 / 2 at GPW 2: 940 / 1,094; R 2 / 4 / 8 at GPW 1: 966 / 1,135 / 1,046.
 #ifndef MM_SB_RROWS
-#define MM_SB_RROWS 2
+#define MM_SB_RROWS 4
 #endif
 constexpr int kSbR = MM_SB_RROWS;
-static_assert(kSbR == 1 || kSbR == 2 || kSbR == 4, "MM_SB_RROWS: 1, 2 or 4");
+static_assert(kSbR == 1 || kSbR == 2 || kSbR == 4 || kSbR == 8, "MM_SB_RROWS: 1, 2, 4 or 8");
 template <int N> __device__ __forceinline__ size_t t_row(int k)   // offset of (k, 0)
 {
     return (size_t)(k / kSbR) * (kSbR * N) + k % kSbR;
