@@ -442,6 +442,20 @@ static int set_attrs(int W)
         // k_sb_cols: exchange buffers (73.7 KB) + its own staging (run_steer)
         HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_cols<12>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        // k_sb_rows: sb_rows_groups<12>() 4096-point transforms (73.7 KB at two)
+        if constexpr (sb_rows_groups<12>() > 1) {
+            const int rl = (int)(sizeof(c2) * sb_rows_groups<12>() * lds_complex<4096>());
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_rows<12, false, 1>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, rl));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_rows<12, false, 2>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, rl));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_rows<12, false, 4>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, rl));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_rows<12, true, 1>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, rl));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sb_rows<12, true, 2>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, rl));
+        }
     }
     if constexpr (LOG2N == 13) {   // N = 8192: one 8192-point transform per workgroup, 73.7 KB and more
         auto set = [](const void *f, size_t b) {
@@ -871,11 +885,13 @@ static int run_steer(mm_handle *h, const uint8_t *in, uint8_t *out, int n, int f
             // bit f: frame k + f's Yh (the stream's first frame passes through)
             const int wmask = write ? (((1 << (ng * nf)) - 1) & ~(reset ? 1 : 0)) : 0;
             ProfScope ps(h, s, MM_K_ROWS_INV, __builtin_popcount(wmask));
-            const dim3 grid((h->geo.Hn + gpw - 1) / gpw), block(wg_threads<LOG2N>());
+            constexpr int rg = sb_rows_groups<LOG2N>();
+            const dim3 grid((h->geo.Hn + rg - 1) / rg), block(sb_rows_threads<LOG2N>());
+            const size_t rlds = sizeof(c2) * (size_t)rg * lds_complex<N>();
             float *yh = h->d_Yh + h->yh_stride * k;
             c2 *tk = h->d_T + t_stride * (k - c0);
 #define MM_SB_ROWS(IIRV, NFV)                                                                              \
-            hipLaunchKernelGGL((k_sb_rows<LOG2N, IIRV, NFV>), grid, block, lds, s, tk, band_stride, t_stride, \
+            hipLaunchKernelGGL((k_sb_rows<LOG2N, IIRV, NFV>), grid, block, rlds, s, tk, band_stride, t_stride, \
                                yh, h->yh_stride, sst, sst + plane, sst + 2 * plane, reset, wmask, h->geo,   \
                                h->spec, h->blur, h->d_tw, ng)
             if (h->spec.filt == MM_FILTER_IIR) {

@@ -1236,6 +1236,18 @@ template <int LOG2N> constexpr int sb_groups() { return groups_at_least<LOG2N, M
 // k_sb_cols with one column per workgroup: the band loop alternates two
 // exchange buffers (the next band's transform never waits for this one's
 // cross-wave reads) and stores from registers (no staging)
+// the steerable band-row kernel: row transforms per workgroup (MM_SB_ROWS2_4K
+// = 1: two at N = 4096, rows k, k+1 of one band-row group reading the same
+// 32-B sectors in one 1,024-thread workgroup: C3 k_sb_rows 465 -> 568 us,
+// profiles/r06h_sb_rows_layout_ab.txt; off)
+#ifndef MM_SB_ROWS2_4K
+#define MM_SB_ROWS2_4K 0
+#endif
+template <int LOG2N> constexpr int sb_rows_groups()
+{
+    return LOG2N == 12 && MM_SB_ROWS2_4K ? 2 : groups_per_wg<LOG2N>();
+}
+template <int LOG2N> constexpr int sb_rows_threads() { return sb_rows_groups<LOG2N>() * fft_T<LOG2N>(); }
 template <int LOG2N> constexpr bool sb_direct() { return MM_SB_GPW1 && sb_groups<LOG2N>() == 1 && fft_c_v(LOG2N) > 1; }
 template <int LOG2N> constexpr int sb_threads() { return sb_groups<LOG2N>() * fft_T<LOG2N>(); }
 // K2's Q staging buffer (c2 slots written by rows, read back as float4

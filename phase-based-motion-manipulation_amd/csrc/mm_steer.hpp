@@ -376,14 +376,17 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 #define MM_SB_IIR_GROUPS 0
 #endif
 template <int LOG2N, bool IIR, int NF>
-__global__ __launch_bounds__(wg_threads<LOG2N>()) __attribute__((amdgpu_waves_per_eu(IIR || NF > 2 ? 4 : 5)))
+__global__ __launch_bounds__(sb_rows_threads<LOG2N>())
+__attribute__((amdgpu_waves_per_eu(IIR || NF > 2 || sb_rows_threads<LOG2N>() >= 1024 ? 4 : 5)))
 void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restrict__ Yh, size_t yh_stride,
                float *st_phi, float *st_uh, float *st_ul,
                int reset, int write_mask, Geo g, Spec sp, Blur5 bw, const c2 *__restrict__ tw, int ngroups)
 {
-    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = groups_per_wg<LOG2N>();
+    constexpr int N = 1 << LOG2N, T = fft_T<LOG2N>(), GPW = sb_rows_groups<LOG2N>();
     extern __shared__ __attribute__((aligned(16))) c2 lds_all[];
-    const int grp = GPW == 1 ? 0 : threadIdx.x / T, t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
+    // (the group index wave-uniform: the row's band and state bases stay scalar)
+    const int grp = GPW == 1 ? 0 : (T % 64 == 0 ? __builtin_amdgcn_readfirstlane(threadIdx.x / T) : threadIdx.x / T);
+    const int t0 = GPW == 1 ? threadIdx.x : threadIdx.x % T;
     c2 *lds = lds_all + grp * lds_complex<N>();
     const int logical = xcd_remap(blockIdx.x, gridDim.x) * GPW + grp;
     const bool valid = logical < g.Hn;
