@@ -96,7 +96,15 @@ template <int LOG2N, int MIN> constexpr int groups_at_least() { return groups_at
 // K3 runs one Q tile (TK = 2 * groups rows) per workgroup
 template <int LOG2N> constexpr int k3_groups() { return groups_at_least<LOG2N, MM_K3_GROUPS>(); }
 template <int LOG2N> constexpr int k3_threads() { return k3_groups<LOG2N>() * fft_T<LOG2N>(); }
-constexpr int q_tile_v(int log2n) { return 2 * groups_at_least_v(log2n, MM_K3_GROUPS); }
+// (MM_Q_TILE_8K: rows per Q tile at N = 8192, where K3 runs one row pair per
+// workgroup: 4 gives K2 32-B Q pieces from its one column per workgroup.
+// 5120x2880 same-call, tiles of 2 / 4 / 8 rows: K2 193-196 / 185 / 179-184 us,
+// K3 31 / 35 / 45 us per frame, 3.04-3.11k / 3.13k / 3.04-3.10k frames/s,
+// profiles/r06k_q_tile_8k_ab.txt)
+#ifndef MM_Q_TILE_8K
+#define MM_Q_TILE_8K 4
+#endif
+constexpr int q_tile_v(int log2n) { return log2n == 13 ? MM_Q_TILE_8K : 2 * groups_at_least_v(log2n, MM_K3_GROUPS); }
 template <int LOG2N> constexpr int q_tile() { return q_tile_v(LOG2N); }
 // K1 runs >= 2 row pairs per workgroup so that G receives 32-B pieces
 template <int LOG2N> constexpr int k1_groups() { return groups_at_least<LOG2N, MM_K1_GROUPS>(); }
