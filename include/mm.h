@@ -205,7 +205,11 @@ void *mm_stream(mm_handle *h);
  * chip across them (each launch first re-transforms the state G_{t-1}).
  * Larger batches amortise that and the launch gaps; the hand-off buffers take
  * about 17.8 MB per 1080p frame (4x at 2160p).  Default: min(64, 2 GiB of
- * buffers).  Results do not depend on the batch size.  Reallocates: the
+ * buffers).  Results do not depend on the batch size.  MM_MODE_STEERABLE
+ * holds, besides, the band rows of one column chunk independent of the batch
+ * (O = 8: 231 MB per 1080p frame x 8 frames, 1.2 GB per 2160p frame x 2; the
+ * MM_SB_CF environment variable, 2..16, sets the 1080p chunk) and the state
+ * planes (100 MB DIFF / 300 MB IIR at 1080p).  Reallocates: the
  * old buffers retire behind this handle's latest work and the call waits for
  * that work only (not for the device, since ABI 9); call between frames.
  * Failure-atomic: on MM_ERR_OOM the handle keeps its previous batch size,
