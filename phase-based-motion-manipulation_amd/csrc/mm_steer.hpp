@@ -375,6 +375,18 @@ void k_sb_cols(const c2 *__restrict__ Fb, c2 *__restrict__ Tb, size_t band_strid
 #ifndef MM_SB_IIR_GROUPS
 #define MM_SB_IIR_GROUPS 0
 #endif
+// k_sb_rows' twiddle bases loaded per band from the (L1-resident) table
+// instead of ~20 VGPRs held across the band loop: IIR (its band loop then
+// fits 128 VGPRs without spills: 1080p O = 8 IIR 4.43k -> 4.52k frames/s,
+// profiles/r06h_sb_rows_layout_ab.txt); MM_SB_TWLD_DIFF for DIFF (at 6 waves
+// per SIMD, 80 VGPRs, it spills 18)
+#ifndef MM_SB_TWLD_IIR
+#define MM_SB_TWLD_IIR 1
+#endif
+#ifndef MM_SB_TWLD_DIFF
+#define MM_SB_TWLD_DIFF 0
+#endif
+template <bool IIR> constexpr bool kSbRowsTwLd = IIR ? MM_SB_TWLD_IIR : MM_SB_TWLD_DIFF;
 template <int LOG2N, bool IIR, int NF>
 __global__ __launch_bounds__(sb_rows_threads<LOG2N>())
 __attribute__((amdgpu_waves_per_eu(IIR || NF > 2 || sb_rows_threads<LOG2N>() >= 1024 ? 4 : 5)))
@@ -400,7 +412,7 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
     c2 wtw[kTwSlots];
 #pragma unroll
     for (int i = 0; i < kTwSlots; ++i) wtw[i] = mk(1.0f, 0.0f);
-    preload_twiddles<LOG2N>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
+    if constexpr (!kSbRowsTwLd<IIR>) preload_twiddles<LOG2N>(wtw, t0, tw);   // forward bases; fft_regs_w conjugates
     // row k of band b of frame f (contiguous) and its state: loaded one row ahead
     c2 v[8];
     float pp[8], puh[8], pul[8];
@@ -470,10 +482,18 @@ void k_sb_rows(const c2 *Tb, size_t band_stride, size_t t_stride, float *__restr
             int t = t0;
             asm volatile("" : "+v"(t));
             c2 wt[kTwSlots];
+            if constexpr (kSbRowsTwLd<IIR>) {
+                // (IIR: the twiddle bases from the L1-resident table per band
+                // instead of ~20 VGPRs held across the band loop)
 #pragma unroll
-            for (int i = 0; i < kTwSlots; ++i) {
-                wt[i] = wtw[i];
-                if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
+                for (int i = 0; i < kTwSlots; ++i) wt[i] = mk(1.0f, 0.0f);
+                preload_twiddles<LOG2N>(wt, t, tw);
+            } else {
+#pragma unroll
+                for (int i = 0; i < kTwSlots; ++i) {
+                    wt[i] = wtw[i];
+                    if (tw_slot_used(LOG2N, i)) asm volatile("" : "+v"(wt[i]));
+                }
             }
             fft_regs_w<LOG2N, +1>(v, t, lds, wt);
             if (b == nb) {   // residual: Hermitian, real output
